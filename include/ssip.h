@@ -1,0 +1,163 @@
+/*
+ * ssip.h — C ABI of libssip_hip.so, the MI355X (gfx950) kernels behind the
+ * semi-supervised ResNet-18 train / pseudo-label / eval / embedding path of
+ * Septimus4/semi-supervised-image-processing.
+ *
+ * The reference has no FFI layer: its hot path is torchvision/torch ops
+ * called from Python.  Each entry point below replaces the op the reference
+ * reaches at the cited call site (paths relative to the reference repo):
+ *
+ *   model(inputs) / loss.backward()        src/training/common.py:380-382
+ *     -> ssip_conv_fwd / _dgrad / _wgrad, ssip_bn_*, ssip_maxpool_*,
+ *        ssip_avgpool_fc_*                  (torchvision resnet18, :299-304)
+ *   criterion(outputs, labels)             src/training/common.py:381
+ *     -> ssip_cross_entropy                (nn.CrossEntropyLoss, semi_supervised.py:111)
+ *   optimizer.step()                       src/training/common.py:383
+ *     -> ssip_adamw                        (optim.AdamW, semi_supervised.py:115-122)
+ *   transform(PIL.Image)                   src/training/common.py:96-119,145,172,192
+ *                                          src/feature_extraction.py:184-207,233-240
+ *     -> ssip_resize_h_u8 + ssip_augment_u8
+ *   softmax/max/threshold pseudo-labels    src/training/semi_supervised.py:57-66
+ *     -> ssip_softmax_select
+ *   (build extension, no reference) weak/strong consistency loss
+ *     -> ssip_semi_loss
+ *
+ * Conventions
+ *   - Every pointer is a device pointer unless documented otherwise; the
+ *     caller owns all memory (kernels never allocate).  Scratch comes from a
+ *     caller buffer sized by the matching *_workspace_bytes / *_floats query.
+ *   - Activations are NHWC, element type selected by `dtype`
+ *     (SSIP_F32 = parity path, SSIP_BF16 = throughput path); all
+ *     accumulation, BatchNorm statistics, weight gradients, optimizer state
+ *     and logits are fp32.
+ *   - `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *     stream-ordered, do no host synchronisation and are safe to capture in
+ *     a hipGraph.
+ *   - Return 0 on success or a negative SSIP_ERR_* code;
+ *     ssip_last_error() returns a thread-local message.  Nothing throws.
+ */
+#ifndef SSIP_H_
+#define SSIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SSIP_ABI_VERSION 1
+
+enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
+enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
+
+const char* ssip_last_error(void);
+int ssip_version(void);
+
+/* ------------------------------------------------------------------------
+ * Convolution as implicit GEMM on MFMA (torchvision nn.Conv2d, bias=False).
+ * x: [N][H][W][C], y/dy: [N][P][Q][K].  C must be a multiple of 32, or C == 4
+ * with S == 8 (the padded 7x7 stem: channel 3 and filter column 7 are zero).
+ * ---------------------------------------------------------------------- */
+typedef struct ssip_conv_desc {
+  int N, H, W, C; /* input (C = stored channels)          */
+  int K;          /* output channels (multiple of 32)      */
+  int R, S;       /* filter rows / stored filter columns   */
+  int stride, pad;
+  int P, Q;       /* output spatial size                   */
+} ssip_conv_desc;
+
+/* floats needed for the BatchNorm partial-statistics buffer of ssip_conv_fwd */
+int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d);
+/* y = conv(x, w); w_krsc: [K][R][S][C] in dtype.  bn_partial (nullable):
+ * fp32 {count, sum, M2} per (M-tile, channel) consumed by ssip_bn_finalize. */
+int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, void* y, float* bn_partial,
+                  void* stream);
+/* dx = conv_transpose(dy, w) (+ dx_add, nullable); w_crsk: [C][R][S][K] */
+int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, void* dx,
+                    const void* dx_add, void* stream);
+int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d);
+/* dw_kcrs (fp32, torchvision layout [K][c_real][R][s_real]) (+)= dW */
+int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
+                    int s_real, int accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * BatchNorm2d (train / eval) fused with ReLU and the residual add.
+ * ---------------------------------------------------------------------- */
+int ssip_bn_finalize(int C, int tiles, const float* partial, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps, int update_running,
+                     float* mean_out, float* invstd_out, float* scale_out, float* shift_out, void* stream);
+int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, float* mean_out, float* invstd_out, float* scale_out,
+                        float* shift_out, void* stream);
+/* z = (relu)(y*scale[c] + shift[c] (+ residual)); M rows of C channels */
+int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
+                  const void* residual, int relu, void* z, void* stream);
+int64_t ssip_bn_bwd_partial_floats(int64_t M, int C);
+/* dout = dz * (zmask > 0) (zmask nullable = no ReLU); dgamma/dbeta (+)= ...;
+ * dy = dBN(dout); dpre (nullable) = dout.  coef: 3*C floats scratch. */
+int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
+                const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
+                void* dpre, float* partial, float* coef, void* stream);
+int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Pooling, head, losses
+ * ---------------------------------------------------------------------- */
+int ssip_maxpool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* x, void* y,
+                     uint8_t* idx, void* stream);
+int ssip_maxpool_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* dy,
+                     const uint8_t* idx, void* dx, void* stream);
+/* feat[b][c] = mean over PQ; logits[b][j] = feat . w[j] + bias[j]  (both fp32, either nullable) */
+int ssip_avgpool_fc_fwd(int dtype, int B, int PQ, int C, int J, const void* z, const float* w, const float* bias,
+                        float* feat, float* logits, void* stream);
+int ssip_avgpool_fc_bwd(int dtype, int B, int PQ, int C, int J, const float* dlogits, const float* w,
+                        const float* feat, void* dz, float* dw, float* dbias, int accumulate, void* stream);
+/* mean CE; dlogits = grad_scale*(softmax - onehot)/B; pred = argmax (each output nullable) */
+int ssip_cross_entropy(int B, int J, const float* logits, const int64_t* labels, float grad_scale, float* loss,
+                       float* dlogits, int64_t* pred, void* stream);
+/* out4 = {total, L_l, L_u, mask_count}:  CE(zl, yl) + lambda * mean_u[1(max softmax zw >= tau) CE(zs, argmax zw)] */
+int ssip_semi_loss(int Bl, int Bu, int J, const float* zl, const int64_t* yl, const float* zw, const float* zs,
+                   float tau, float lambda_u, float* out4, float* dzl, float* dzs, int64_t* pseudo, uint8_t* mask,
+                   void* stream);
+int ssip_softmax_select(int B, int J, const float* logits, float threshold, int pos_col, float* probs, float* conf,
+                        int64_t* pred, uint8_t* keep, float* pos_prob, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Input pipeline (Pillow-exact).  Images are uint8 RGB [B][H][W][3].
+ * ---------------------------------------------------------------------- */
+typedef struct ssip_aug_param {
+  int32_t flip;                       /* horizontal flip before rotation             */
+  int32_t rotate;                     /* 1: Pillow 16.16 affine walk below           */
+  int32_t a0, a1, a3, a4, xo, yo;     /* ImagingTransformAffine fixed-point terms    */
+  int32_t photometric;                /* 1: brightness/contrast jitter (strong view) */
+  float brightness, contrast;
+  int32_t cut_x0, cut_y0, cut_x1, cut_y1; /* cutout box set to 0.5 (empty if x1<=x0) */
+  int32_t reserved;
+} ssip_aug_param;
+
+/* horizontal resample pass: tmp [B][Hs][Wo][3]; bounds [Wo][2] = {xmin, count}; coeffs [Wo][ksize] (22-bit) */
+int ssip_resize_h_u8(int B, const uint8_t* src, int64_t src_batch_stride, int Hs, int Ws, int Wo, int ksize,
+                     const int* bounds, const int* coeffs, uint8_t* tmp, void* stream);
+/* vertical pass (ksize_v > 0) or none, then flip/rotate/photometric/cutout in the Hr x Wr frame,
+ * crop (crop_x, crop_y, Wo, Ho), ToTensor + Normalize -> out [B][Ho][Wo][4] (channel 3 = 0).
+ * mean3/std3 are HOST pointers; params (nullable) is a device array of B entries. */
+int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stride, int src_h, int src_w, int Hr,
+                    int Wr, int Ho, int Wo, int crop_x, int crop_y, int ksize_v, const int* bounds_v,
+                    const int* coeffs_v, const ssip_aug_param* params, const float* mean3, const float* std3,
+                    void* out, void* stream);
+/* f32 NCHW (the nn.Module input contract) -> NHWC with Cp >= C channels */
+int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, const float* x, void* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Optimizer and weight preparation
+ * ---------------------------------------------------------------------- */
+int ssip_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
+               float beta2, float eps, float weight_decay, int64_t step, float grad_scale, void* stream);
+/* w_kcrs (fp32 torchvision layout) -> w_krsc [K][R][Sp][Cp] and/or w_crsk [Cp][R][Sp][K] in dtype */
+int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, const float* w_kcrs, void* w_krsc,
+                     void* w_crsk, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SSIP_H_ */

@@ -1,0 +1,354 @@
+// BatchNorm2d (training + eval) for NHWC activations, with the ReLU and the
+// BasicBlock residual add fused into the elementwise passes.
+//
+// Reference semantics (torchvision resnet18 BatchNorm2d, used through
+// `model(inputs)` at src/training/common.py:380 and `model.train()` at :371):
+// batch mean / biased variance normalise, running_var gets the unbiased
+// variance, momentum 0.1, eps 1e-5.  In the frozen-backbone pretrain stage
+// (src/training/semi_supervised.py:260-285) BN still runs in train mode, so
+// the running statistics keep updating even though gamma/beta are frozen.
+//
+// Statistics: the conv FWD epilogue already produced per-(tile, channel)
+// {count, sum, M2} records; `bn_finalize` merges them in fixed order in
+// fp64 (two-pass: global mean, then sum of M2_t + n_t (mean_t - mean)^2).
+// Backward: `bn_bwd_reduce` computes per-(row-block, channel) partial sums
+// of dout and dout*xhat (dout = dz masked by the following ReLU), the
+// finalize merges them in fp64, `bn_bwd_apply` writes
+// dy = A*dout + B*y + Cc  (per-channel A, B, Cc) and optionally dout itself
+// (the gradient that flows down the identity branch).
+#include "ssip_common.h"
+
+namespace {
+
+__global__ void bn_finalize_kernel(int C, int tiles, const float* __restrict__ partial, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* running_mean, float* running_var,
+                                   float momentum, float eps, int update_running, float* mean_out,
+                                   float* invstd_out, float* scale_out, float* shift_out) {
+  const int c = blockIdx.x;
+  __shared__ double red[256];
+  __shared__ double s_mean, s_n;
+  double n = 0.0, sum = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+    const float* rec = partial + ((long)c * tiles + t) * 3;
+    n += rec[0];
+    sum += rec[1];
+  }
+  // reduce n
+  red[threadIdx.x] = n;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) s_n = red[0];
+  __syncthreads();
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) s_mean = red[0] / s_n;
+  __syncthreads();
+  const double mean = s_mean, N = s_n;
+  double m2 = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
+    const float* rec = partial + ((long)c * tiles + t) * 3;
+    const double nt = rec[0];
+    if (nt > 0) {
+      const double d = (double)rec[1] / nt - mean;
+      m2 += (double)rec[2] + nt * d * d;
+    }
+  }
+  red[threadIdx.x] = m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double var = red[0] / N;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float scale = g * invstd;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    scale_out[c] = scale;
+    shift_out[c] = b - (float)mean * scale;
+    if (update_running) {
+      const double unbiased = N > 1 ? red[0] / (N - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+    }
+  }
+}
+
+__global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                                      float eps, float* mean_out, float* invstd_out, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - rm[c] * g * invstd;
+  if (mean_out) mean_out[c] = rm[c];
+  if (invstd_out) invstd_out[c] = invstd;
+}
+
+// z = act(y*scale + shift (+ residual)), 8 channels per thread.  The grid
+// stride is a multiple of C/8 (blockDim 256, C/8 | 256), so each thread keeps
+// one channel chunk and its scale/shift in registers.
+template <typename T>
+__global__ void bn_apply_kernel(int total8, int C, const T* __restrict__ y, const float* __restrict__ scale,
+                                const float* __restrict__ shift, const T* __restrict__ res, int relu,
+                                T* __restrict__ z) {
+  const int cpr = C >> 3;
+  const int start = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (start % cpr) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = start; i < total8; i += stride) {
+    Vec8<T> v, r, o;
+    v.load(y + (long)i * 8);
+    if (res) r.load(res + (long)i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v.get(j) * sc[j] + sh[j];
+      if (res) t += r.get(j);
+      if (relu) t = t > 0.f ? t : 0.f;
+      o.set(j, t);
+    }
+    o.store(z + (long)i * 8);
+  }
+}
+
+// per-(row block, channel) sums of dout and dout*xhat.
+// Block: 256 threads; each thread owns an 8-channel chunk; threads/row = C/8.
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T* __restrict__ dz,
+                                     const T* __restrict__ zmask, const T* __restrict__ y,
+                                     const float* __restrict__ mean, const float* __restrict__ invstd,
+                                     float* __restrict__ partial) {
+  const int cpr = C / 8;               // chunks per row
+  const int rpi = 256 / cpr;           // rows per iteration (>= 1 since C <= 2048)
+  const int chunk = threadIdx.x % cpr;
+  const int rsub = threadIdx.x / cpr;
+  const int c0 = chunk * 8;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float sd[8], sx[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sd[j] = 0.f; sx[j] = 0.f; mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j];
+  }
+  if (rsub < rpi) {
+    for (long r = r0 + rsub; r < r1; r += rpi) {
+      Vec8<T> g, zz, yy;
+      g.load(dz + r * C + c0);
+      yy.load(y + r * C + c0);
+      if (zmask) zz.load(zmask + r * C + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = g.get(j);
+        if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
+        const float xh = (yy.get(j) - mu[j]) * is[j];
+        sd[j] += d;
+        sx[j] += d * xh;
+      }
+    }
+  }
+  __shared__ float red[2][256][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x][j] = sd[j];
+    red[1][threadIdx.x][j] = sx[j];
+  }
+  __syncthreads();
+  // threads with rsub == 0 sum over rsub in fixed order
+  if (threadIdx.x < cpr) {
+    float* out = partial + ((long)blockIdx.x * C + c0) * 2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = 0.f, b = 0.f;
+      for (int s = 0; s < rpi; ++s) {
+        a += red[0][s * cpr + threadIdx.x][j];
+        b += red[1][s * cpr + threadIdx.x][j];
+      }
+      out[2 * j] = a;
+      out[2 * j + 1] = b;
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(int C, int blocks, long M, const float* __restrict__ partial,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* dgamma, float* dbeta,
+                                       int accumulate, float* coef) {
+  const int c = blockIdx.x;
+  __shared__ double r0[256], r1[256];
+  double a = 0.0, b = 0.0;
+  for (int t = threadIdx.x; t < blocks; t += blockDim.x) {
+    a += partial[((long)t * C + c) * 2 + 0];
+    b += partial[((long)t * C + c) * 2 + 1];
+  }
+  r0[threadIdx.x] = a;
+  r1[threadIdx.x] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      r0[threadIdx.x] += r0[threadIdx.x + o];
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double sum_d = r0[0], sum_dx = r1[0];
+    if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + sum_dx : sum_dx);
+    if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + sum_d : sum_d);
+    const double g = gamma ? gamma[c] : 1.0;
+    const double is = invstd[c];
+    const double A = g * is;
+    const double k0 = -A * sum_d / (double)M;
+    const double k1 = -A * sum_dx / (double)M * is;
+    coef[c] = (float)A;                       // * dout
+    coef[C + c] = (float)k1;                  // * y
+    coef[2 * C + c] = (float)(k0 - k1 * mean[c]);  // constant
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz, const T* __restrict__ zmask,
+                                    const T* __restrict__ y, const float* __restrict__ coef, T* __restrict__ dy,
+                                    T* __restrict__ dpre) {
+  const int cpr = C >> 3;
+  const int start = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (start % cpr) * 8;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j]; }
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = start; i < total8; i += stride) {
+    Vec8<T> g, zz, yy, o, p;
+    g.load(dz + (long)i * 8);
+    yy.load(y + (long)i * 8);
+    if (zmask) zz.load(zmask + (long)i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float d = g.get(j);
+      if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
+      p.set(j, d);
+      o.set(j, ca[j] * d + cb[j] * yy.get(j) + cc[j]);
+    }
+    o.store(dy + (long)i * 8);
+    if (dpre) p.store(dpre + (long)i * 8);
+  }
+}
+
+// dst = src * (mask > 0)  (ReLU backward as a standalone pass)
+template <typename T>
+__global__ void relu_bwd_kernel(long total8, const T* __restrict__ g, const T* __restrict__ z, T* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8; i += (long)gridDim.x * blockDim.x) {
+    Vec8<T> a, m, o;
+    a.load(g + i * 8);
+    m.load(z + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.set(j, m.get(j) > 0.f ? a.get(j) : 0.f);
+    o.store(out + i * 8);
+  }
+}
+
+static int grid_for(long n, int per_block = 256) {
+  long b = (n + per_block - 1) / per_block;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+static int bwd_rows_per_block(long M, int C) {
+  // aim for ~1024 blocks, at least one full iteration of rows
+  const int rpi = 256 / (C / 8);
+  long rows = (M + 1023) / 1024;
+  if (rows < rpi) rows = rpi;
+  rows = ((rows + rpi - 1) / rpi) * rpi;
+  return (int)rows;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ssip_bn_finalize(int C, int tiles, const float* partial, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps, int update_running,
+                     float* mean_out, float* invstd_out, float* scale_out, float* shift_out, void* stream) {
+  SSIP_REQUIRE(C > 0 && tiles > 0 && partial && mean_out && invstd_out && scale_out && shift_out, SSIP_ERR_ARG,
+               "ssip_bn_finalize: bad arguments");
+  SSIP_REQUIRE(!update_running || (running_mean && running_var), SSIP_ERR_ARG, "running stats required");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, C, tiles, partial, gamma, beta,
+                     running_mean, running_var, momentum, eps, update_running, mean_out, invstd_out, scale_out,
+                     shift_out);
+  return ::ssip::check_launch("bn_finalize");
+}
+
+int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, float* mean_out, float* invstd_out, float* scale_out,
+                        float* shift_out, void* stream) {
+  SSIP_REQUIRE(C > 0 && running_mean && running_var && scale_out && shift_out, SSIP_ERR_ARG,
+               "ssip_bn_eval_coeffs: bad arguments");
+  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, gamma, beta,
+                     running_mean, running_var, eps, mean_out, invstd_out, scale_out, shift_out);
+  return ::ssip::check_launch("bn_eval_coeffs");
+}
+
+int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
+                  const void* residual, int relu, void* z, void* stream) {
+  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && y && scale && shift && z, SSIP_ERR_ARG, "ssip_bn_apply: bad arguments");
+  SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply: unsupported size");
+  const int total8 = (int)(M * C / 8);
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, (hipStream_t)stream, total8, C,
+                       (const T*)y, scale, shift, (const T*)residual, relu, (T*)z);
+  });
+  return ::ssip::check_launch("bn_apply");
+}
+
+int64_t ssip_bn_bwd_partial_floats(int64_t M, int C) {
+  if (M <= 0 || C <= 0 || C % 8 || C > 2048) return -1;
+  const int rows = bwd_rows_per_block(M, C);
+  return ((M + rows - 1) / rows) * (int64_t)C * 2;
+}
+
+int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
+                const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
+                void* dpre, float* partial, float* coef, void* stream) {
+  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= 2048 && dz && y && mean && invstd && dy && partial && coef,
+               SSIP_ERR_ARG, "ssip_bn_bwd: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = bwd_rows_per_block(M, C);
+  const int blocks = (int)((M + rows - 1) / rows);
+  SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_bwd: unsupported size");
+  const int total8 = (int)(M * C / 8);
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
+                       (const T*)zmask, (const T*)y, mean, invstd, partial);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, C, blocks, (long)M, partial, gamma, mean,
+                       invstd, dgamma, dbeta, accumulate, coef);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
+                       (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre);
+  });
+  return ::ssip::check_launch("bn_bwd");
+}
+
+int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream) {
+  SSIP_REQUIRE(n > 0 && n % 8 == 0 && g && z && out, SSIP_ERR_ARG, "ssip_relu_bwd: bad arguments");
+  const long total8 = n / 8;
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(relu_bwd_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, (hipStream_t)stream, total8,
+                       (const T*)g, (const T*)z, (T*)out);
+  });
+  return ::ssip::check_launch("relu_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+"""ctypes binding of libssip_hip.so (the C ABI declared in include/ssip.h).
+
+This is the only place Python touches the native library.  Every call
+checks the returned status and raises ``RuntimeError`` with
+``ssip_last_error()``; a missing library raises at first use — there is
+no CPU fallback in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("SSIP_LIB", _HERE / "libssip_hip.so"))
+
+F32 = 0
+BF16 = 1
+
+_c_int = ctypes.c_int
+_c_i64 = ctypes.c_int64
+_c_f = ctypes.c_float
+_vp = ctypes.c_void_p
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("N", "H", "W", "C", "K", "R", "S", "stride", "pad", "P", "Q")]
+
+
+class AugParam(ctypes.Structure):
+    _fields_ = [
+        ("flip", ctypes.c_int32),
+        ("rotate", ctypes.c_int32),
+        ("a0", ctypes.c_int32),
+        ("a1", ctypes.c_int32),
+        ("a3", ctypes.c_int32),
+        ("a4", ctypes.c_int32),
+        ("xo", ctypes.c_int32),
+        ("yo", ctypes.c_int32),
+        ("photometric", ctypes.c_int32),
+        ("brightness", ctypes.c_float),
+        ("contrast", ctypes.c_float),
+        ("cut_x0", ctypes.c_int32),
+        ("cut_y0", ctypes.c_int32),
+        ("cut_x1", ctypes.c_int32),
+        ("cut_y1", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+_PD = ctypes.POINTER(ConvDesc)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "ssip_last_error": (ctypes.c_char_p, []),
+    "ssip_version": (_c_int, []),
+    "ssip_conv_fwd_partial_floats": (_c_i64, [_PD]),
+    "ssip_conv_fwd": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_conv_dgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_conv_wgrad_workspace_bytes": (_c_i64, [_PD]),
+    "ssip_conv_wgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _vp]),
+    "ssip_bn_finalize": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_bn_eval_coeffs": (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_bn_apply": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
+    "ssip_bn_bwd_partial_floats": (_c_i64, [_c_i64, _c_int]),
+    "ssip_bn_bwd": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_relu_bwd": (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp]),
+    "ssip_maxpool_fwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),
+    "ssip_maxpool_bwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),
+    "ssip_avgpool_fc_fwd": (_c_int, [_c_int] * 5 + [_vp] * 6),
+    "ssip_avgpool_fc_bwd": (_c_int, [_c_int] * 5 + [_vp] * 6 + [_c_int, _vp]),
+    "ssip_cross_entropy": (_c_int, [_c_int, _c_int, _vp, _vp, _c_f, _vp, _vp, _vp, _vp]),
+    "ssip_semi_loss": (_c_int, [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_f, _c_f, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_softmax_select": (_c_int, [_c_int, _c_int, _vp, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_resize_h_u8": (_c_int, [_c_int, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp]),
+    "ssip_augment_u8": (
+        _c_int,
+        [_c_int, _c_int, _vp, _c_i64] + [_c_int] * 9 + [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    ),
+    "ssip_nchw_to_nhwc": (_c_int, [_c_int] * 6 + [_vp, _vp, _vp]),
+    "ssip_adamw": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_f, _vp]),
+    "ssip_weight_prep": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp, _vp]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"ssip native library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)"
+            )
+        handle = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ssip_last_error().decode("utf-8", "replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name: str, *args) -> int:
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if _SIGS[name][0] is _c_int and name not in ("ssip_version",):
+        check(rc, name)
+    return rc

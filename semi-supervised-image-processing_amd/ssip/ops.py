@@ -1,0 +1,228 @@
+"""Tensor-level wrappers over the C ABI (include/ssip.h).
+
+Each function takes torch tensors that already live on the HIP device,
+checks shapes/dtypes on the host, and launches on the current torch stream.
+No function here falls back to a torch op.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import ConvDesc, call
+
+_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"ssip: unsupported activation dtype {t.dtype}") from None
+
+
+def _p(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("ssip: tensor must be on the HIP device")
+    if not t.is_contiguous():
+        raise ValueError("ssip: tensor must be contiguous")
+    return t.data_ptr()
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ---------------------------------------------------------------------------
+# convolution
+# ---------------------------------------------------------------------------
+@dataclass(frozen=True)
+class ConvGeom:
+    N: int
+    H: int
+    W: int
+    C: int  # stored input channels (4 for the padded stem)
+    K: int
+    R: int
+    S: int  # stored filter columns (8 for the padded stem)
+    stride: int
+    pad: int
+    c_real: int
+    s_real: int
+
+    @property
+    def P(self) -> int:
+        return (self.H + 2 * self.pad - self.R) // self.stride + 1
+
+    @property
+    def Q(self) -> int:
+        return (self.W + 2 * self.pad - self.s_real) // self.stride + 1
+
+    def desc(self) -> ConvDesc:
+        # the padded stem column (s = 7) must not change the output width:
+        # Q is computed with the real filter width; the kernel only needs P/Q.
+        d = ConvDesc(self.N, self.H, self.W, self.C, self.K, self.R, self.S, self.stride, self.pad, self.P, self.Q)
+        return d
+
+    def flops(self) -> int:
+        return 2 * self.N * self.P * self.Q * self.K * self.c_real * self.R * self.s_real
+
+
+def conv_fwd_partial_floats(g: ConvGeom) -> int:
+    return int(_lib.lib().ssip_conv_fwd_partial_floats(g.desc()))
+
+
+def conv_fwd(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor,
+             partial: Optional[torch.Tensor] = None) -> None:
+    assert x.numel() == g.N * g.H * g.W * g.C, "conv_fwd: x shape"
+    assert w_krsc.numel() == g.K * g.R * g.S * g.C, "conv_fwd: w shape"
+    assert y.numel() == g.N * g.P * g.Q * g.K, "conv_fwd: y shape"
+    assert x.dtype == w_krsc.dtype == y.dtype
+    if partial is not None:
+        assert partial.dtype == torch.float32 and partial.numel() >= conv_fwd_partial_floats(g)
+    d = g.desc()
+    call("ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial), stream_ptr())
+
+
+def conv_dgrad(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx: torch.Tensor,
+               dx_add: Optional[torch.Tensor] = None) -> None:
+    assert dy.numel() == g.N * g.P * g.Q * g.K, "conv_dgrad: dy shape"
+    assert w_crsk.numel() == g.K * g.R * g.S * g.C, "conv_dgrad: w shape"
+    assert dx.numel() == g.N * g.H * g.W * g.C, "conv_dgrad: dx shape"
+    if dx_add is not None:
+        assert dx_add.numel() == dx.numel() and dx_add.dtype == dx.dtype
+    call("ssip_conv_dgrad", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx), _p(dx_add), stream_ptr())
+
+
+def conv_wgrad_workspace_bytes(g: ConvGeom) -> int:
+    return int(_lib.lib().ssip_conv_wgrad_workspace_bytes(g.desc()))
+
+
+def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool,
+               workspace: torch.Tensor) -> None:
+    assert dy.numel() == g.N * g.P * g.Q * g.K and x.numel() == g.N * g.H * g.W * g.C
+    assert dw.dtype == torch.float32 and dw.numel() == g.K * g.c_real * g.R * g.s_real
+    nbytes = workspace.numel() * workspace.element_size()
+    call("ssip_conv_wgrad", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real, int(accumulate),
+         _p(workspace), nbytes, stream_ptr())
+
+
+def weight_prep(w: torch.Tensor, dtype: torch.dtype, Cp: int, Sp: int, krsc: Optional[torch.Tensor],
+                crsk: Optional[torch.Tensor]) -> None:
+    K, C, R, S = w.shape
+    call("ssip_weight_prep", _DT[dtype], K, C, R, S, Cp, Sp, _p(w), _p(krsc), _p(crsk), stream_ptr())
+
+
+# ---------------------------------------------------------------------------
+# batch norm
+# ---------------------------------------------------------------------------
+def bn_finalize(C: int, tiles: int, partial, gamma, beta, running_mean, running_var, momentum: float, eps: float,
+                update_running: bool, mean, invstd, scale, shift) -> None:
+    call("ssip_bn_finalize", C, tiles, _p(partial), _p(gamma), _p(beta), _p(running_mean), _p(running_var),
+         float(momentum), float(eps), int(update_running), _p(mean), _p(invstd), _p(scale), _p(shift), stream_ptr())
+
+
+def bn_eval_coeffs(C: int, gamma, beta, running_mean, running_var, eps: float, mean, invstd, scale, shift) -> None:
+    call("ssip_bn_eval_coeffs", C, _p(gamma), _p(beta), _p(running_mean), _p(running_var), float(eps), _p(mean),
+         _p(invstd), _p(scale), _p(shift), stream_ptr())
+
+
+def bn_apply(M: int, C: int, y, scale, shift, residual, relu: bool, z) -> None:
+    call("ssip_bn_apply", dtype_code(y), M, C, _p(y), _p(scale), _p(shift), _p(residual), int(relu), _p(z),
+         stream_ptr())
+
+
+def bn_bwd_partial_floats(M: int, C: int) -> int:
+    return int(_lib.lib().ssip_bn_bwd_partial_floats(M, C))
+
+
+def bn_bwd(M: int, C: int, dz, zmask, y, mean, invstd, gamma, dgamma, dbeta, accumulate: bool, dy, dpre, partial,
+           coef) -> None:
+    call("ssip_bn_bwd", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(y), _p(mean), _p(invstd), _p(gamma),
+         _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(dpre), _p(partial), _p(coef), stream_ptr())
+
+
+def relu_bwd(g, z, out) -> None:
+    call("ssip_relu_bwd", dtype_code(g), g.numel(), _p(g), _p(z), _p(out), stream_ptr())
+
+
+# ---------------------------------------------------------------------------
+# pooling / head / losses
+# ---------------------------------------------------------------------------
+def maxpool_fwd(N, H, W, C, k, s, pad, x, y, idx) -> None:
+    call("ssip_maxpool_fwd", dtype_code(x), N, H, W, C, k, s, pad, _p(x), _p(y), _p(idx), stream_ptr())
+
+
+def maxpool_bwd(N, H, W, C, k, s, pad, dy, idx, dx) -> None:
+    call("ssip_maxpool_bwd", dtype_code(dy), N, H, W, C, k, s, pad, _p(dy), _p(idx), _p(dx), stream_ptr())
+
+
+def avgpool_fc_fwd(B, PQ, C, J, z, w, bias, feat, logits) -> None:
+    call("ssip_avgpool_fc_fwd", dtype_code(z), B, PQ, C, J, _p(z), _p(w), _p(bias), _p(feat), _p(logits),
+         stream_ptr())
+
+
+def avgpool_fc_bwd(dtype: torch.dtype, B, PQ, C, J, dlogits, w, feat, dz, dw, dbias, accumulate: bool) -> None:
+    call("ssip_avgpool_fc_bwd", _DT[dtype], B, PQ, C, J, _p(dlogits), _p(w), _p(feat), _p(dz), _p(dw), _p(dbias),
+         int(accumulate), stream_ptr())
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, grad_scale: float = 1.0, want_grad: bool = True):
+    """Returns (loss[1], dlogits or None, pred[B]) — all device tensors."""
+    B, J = logits.shape
+    logits = logits.contiguous().float()
+    labels = labels.contiguous().to(torch.int64)
+    loss = torch.empty(1, device=logits.device, dtype=torch.float32)
+    dl = torch.empty_like(logits) if want_grad else None
+    pred = torch.empty(B, device=logits.device, dtype=torch.int64)
+    call("ssip_cross_entropy", B, J, _p(logits), _p(labels), float(grad_scale), _p(loss), _p(dl), _p(pred),
+         stream_ptr())
+    return loss, dl, pred
+
+
+def semi_loss(zl, yl, zw, zs, tau: float, lambda_u: float):
+    Bl = 0 if zl is None else zl.shape[0]
+    Bu = 0 if zw is None else zw.shape[0]
+    J = (zl if zl is not None else zw).shape[1]
+    dev = (zl if zl is not None else zw).device
+    out = torch.empty(4, device=dev, dtype=torch.float32)
+    dzl = torch.empty_like(zl) if zl is not None else None
+    dzs = torch.empty_like(zs) if zs is not None else None
+    pseudo = torch.empty(Bu, device=dev, dtype=torch.int64) if Bu else None
+    mask = torch.empty(Bu, device=dev, dtype=torch.uint8) if Bu else None
+    call("ssip_semi_loss", Bl, Bu, J, _p(zl), _p(yl), _p(zw), _p(zs), float(tau), float(lambda_u), _p(out), _p(dzl),
+         _p(dzs), _p(pseudo), _p(mask), stream_ptr())
+    return out, dzl, dzs, pseudo, mask
+
+
+def softmax_select(logits: torch.Tensor, threshold: float = 0.0, pos_col: int = 0):
+    """softmax, max, argmax, (max >= threshold), P(pos_col) in one launch."""
+    B, J = logits.shape
+    logits = logits.contiguous().float()
+    dev = logits.device
+    probs = torch.empty_like(logits)
+    conf = torch.empty(B, device=dev, dtype=torch.float32)
+    pred = torch.empty(B, device=dev, dtype=torch.int64)
+    keep = torch.empty(B, device=dev, dtype=torch.uint8)
+    pos = torch.empty(B, device=dev, dtype=torch.float32)
+    call("ssip_softmax_select", B, J, _p(logits), float(threshold), int(pos_col), _p(probs), _p(conf), _p(pred),
+         _p(keep), _p(pos), stream_ptr())
+    return probs, conf, pred, keep, pos
+
+
+def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0) -> None:
+    call("ssip_adamw", param.numel(), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), float(lr), float(beta1),
+         float(beta2), float(eps), float(weight_decay), int(step), float(grad_scale), stream_ptr())
+
+
+def nchw_to_nhwc(x: torch.Tensor, Cp: int, dtype: torch.dtype) -> torch.Tensor:
+    B, C, H, W = x.shape
+    x = x.contiguous().float()
+    out = torch.empty((B, H, W, Cp), device=x.device, dtype=dtype)
+    call("ssip_nchw_to_nhwc", _DT[dtype], B, C, H, W, Cp, _p(x), _p(out), stream_ptr())
+    return out

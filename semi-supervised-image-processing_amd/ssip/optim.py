@@ -1,0 +1,90 @@
+"""Fused AdamW (torch.optim.AdamW semantics) on the flat parameter arena.
+
+Drop-in for ``optim.AdamW(params, lr, weight_decay)`` as built by the
+reference (src/training/semi_supervised.py:115-122, 265-272, 291-298;
+src/training/supervised.py:71-78).  Parameters that live in a
+``ParamArena`` are updated by ONE ``ssip_adamw`` launch per contiguous run
+of trainable parameters; any other parameter gets its own launch.  The
+state layout (``step``, ``exp_avg``, ``exp_avg_sq`` per parameter) and
+``param_groups`` match torch's, so ``ReduceLROnPlateau`` and
+``state_dict()`` work unchanged.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Tuple
+
+import torch
+
+from . import ops
+
+
+class AdamW(torch.optim.Optimizer):
+    def __init__(self, params: Iterable, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 1e-2, arena=None):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.arena = arena
+        self._flat_state = None  # (exp_avg_flat, exp_avg_sq_flat) parallel to arena.flat
+        self._runs_cache: Dict[int, List[Tuple[int, int, List[torch.Tensor]]]] = {}
+
+    def _ensure_flat_state(self):
+        if self.arena is not None and self._flat_state is None:
+            self._flat_state = (torch.zeros_like(self.arena.flat), torch.zeros_like(self.arena.flat))
+
+    def _runs(self, gi: int, params: List[torch.Tensor]):
+        """Group arena-resident params of a group into contiguous runs."""
+        spans = []
+        loose = []
+        for p in params:
+            if self.arena is not None and self.arena.owns(p) and p.grad is not None and \
+                    p.grad.data_ptr() == self.arena.grad_view(p).data_ptr():
+                off, n = self.arena.span(p)
+                spans.append((off, n, p))
+            else:
+                loose.append(p)
+        spans.sort(key=lambda t: t[0])
+        runs: List[Tuple[int, int, List[torch.Tensor]]] = []
+        for off, n, p in spans:
+            if runs and runs[-1][0] + runs[-1][1] == off:
+                o0, n0, ps = runs[-1]
+                runs[-1] = (o0, n0 + n, ps + [p])
+            else:
+                runs.append((off, n, [p]))
+        return runs, loose
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._ensure_flat_state()
+        for gi, group in enumerate(self.param_groups):
+            b1, b2 = group["betas"]
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            runs, loose = self._runs(gi, params)
+            # per-parameter state (views into the flat state for arena params)
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    if self._flat_state is not None and self.arena.owns(p):
+                        off, n = self.arena.span(p)
+                        st["exp_avg"] = self._flat_state[0][off:off + n].view_as(p)
+                        st["exp_avg_sq"] = self._flat_state[1][off:off + n].view_as(p)
+                    else:
+                        st["exp_avg"] = torch.zeros_like(p)
+                        st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+            for off, n, ps in runs:
+                step = int(self.state[ps[0]]["step"].item())
+                ops.adamw(self.arena.flat[off:off + n], self.arena.grad[off:off + n],
+                          self._flat_state[0][off:off + n], self._flat_state[1][off:off + n],
+                          group["lr"], b1, b2, group["eps"], group["weight_decay"], step)
+            for p in loose:
+                st = self.state[p]
+                ops.adamw(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
+                          group["eps"], group["weight_decay"], int(st["step"].item()))
+        return loss

@@ -1,0 +1,543 @@
+"""ResNet-18/50 on the ssip HIP kernels, behind the torchvision module API.
+
+Reference boundary: `create_model` (src/training/common.py:299-304) returns a
+torchvision ``resnet18`` whose ``fc`` is replaced by ``nn.Linear(512, C)``;
+the train loop calls ``model(inputs)`` with f32 NCHW batches
+(common.py:380), ``loss.backward()`` (:382) and ``optimizer.step()``
+(:383); checkpoints are ``model.state_dict()`` (:418-424) with torchvision
+key names; feature extraction uses ``children()[:-1]`` = everything up to
+the global average pool (src/feature_extraction.py:210-227).
+
+Design (MI355X-first):
+  * The nn.Module tree below is a *parameter container* that mirrors
+    torchvision's construction order exactly (same RNG consumption, same
+    state_dict keys/shapes), so seeded initialisation and checkpoints are
+    interchangeable with torchvision's.  Its submodules are never called.
+  * ``forward`` runs the whole network as ONE autograd node whose forward
+    and backward are sequences of C-ABI launches (libssip_hip.so) on NHWC
+    activations in bf16 or f32; weight gradients are written straight into
+    ``param.grad`` (views into one flat fp32 arena when the model is
+    flattened for the fused optimizer / RCCL all-reduce).
+  * BatchNorm semantics follow torch: train mode uses batch statistics and
+    updates running stats (also in the frozen-backbone stage,
+    src/training/semi_supervised.py:260-285), eval mode uses running stats.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .ops import ConvGeom
+
+# ---------------------------------------------------------------------------
+# parameter containers (torchvision-compatible structure and init order)
+# ---------------------------------------------------------------------------
+
+
+def _conv3x3(i, o, stride=1):
+    return nn.Conv2d(i, o, kernel_size=3, stride=stride, padding=1, bias=False)
+
+
+def _conv1x1(i, o, stride=1):
+    return nn.Conv2d(i, o, kernel_size=1, stride=stride, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = _conv3x3(inplanes, planes, stride)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = _conv3x3(planes, planes)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def stages(self):
+        return [(self.conv1, self.bn1), (self.conv2, self.bn2)]
+
+    def forward(self, x):  # pragma: no cover - containers are never executed
+        raise RuntimeError("ssip blocks are parameter containers; call the top-level model")
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        width = planes
+        self.conv1 = _conv1x1(inplanes, width)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = _conv3x3(width, width, stride)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = _conv1x1(width, planes * self.expansion)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def stages(self):
+        return [(self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)]
+
+    def forward(self, x):  # pragma: no cover
+        raise RuntimeError("ssip blocks are parameter containers; call the top-level model")
+
+
+ARCHS = {
+    "resnet18": (BasicBlock, [2, 2, 2, 2]),
+    "resnet34": (BasicBlock, [3, 4, 6, 3]),
+    "resnet50": (Bottleneck, [3, 4, 6, 3]),
+}
+
+_DTYPES = {"fp32": torch.float32, "f32": torch.float32, "float32": torch.float32,
+           "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+@dataclass
+class DeviceImages:
+    """A batch already in the stem's NHWC4 layout and the engine dtype
+    (produced by ``ssip.augment``): skips the NCHW->NHWC conversion."""
+
+    nhwc4: torch.Tensor
+
+    def __len__(self):
+        return self.nhwc4.shape[0]
+
+
+class _Identity(nn.Module):
+    def forward(self, x):
+        return x
+
+
+# ---------------------------------------------------------------------------
+# saved forward state
+# ---------------------------------------------------------------------------
+@dataclass
+class _ConvRec:
+    geom: ConvGeom
+    conv: nn.Conv2d
+    bn: nn.BatchNorm2d
+    x: torch.Tensor          # conv input  [N,H,W,C]
+    y: torch.Tensor          # conv output [N,P,Q,K] (pre-BN)
+    stats: torch.Tensor      # [4, K] mean, invstd, scale, shift
+    z: Optional[torch.Tensor] = None   # post BN(+add)+ReLU output (mask source)
+
+
+@dataclass
+class _Saved:
+    dtype: torch.dtype
+    N: int
+    stem: _ConvRec = None
+    pool_out: torch.Tensor = None
+    pool_idx: torch.Tensor = None
+    pool_hw: Tuple[int, int] = (0, 0)
+    blocks: List[Tuple[List[_ConvRec], Optional[_ConvRec], torch.Tensor]] = field(default_factory=list)
+    feat: torch.Tensor = None
+    logits: Optional[torch.Tensor] = None
+    last: torch.Tensor = None
+    last_pq: int = 0
+
+
+class SSIPResNet(nn.Module):
+    """torchvision-compatible ResNet whose compute runs on libssip_hip.so."""
+
+    def __init__(self, arch: str = "resnet18", num_classes: int = 1000, dtype: str = "fp32"):
+        super().__init__()
+        block, layers = ARCHS[arch]
+        self.arch = arch
+        self.inplanes = 64
+        self.dilation = 1
+        self.groups = 1
+        self.base_width = 64
+        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(self.inplanes)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+        self.compute_dtype = _DTYPES[dtype]
+        self.bn_update_running = True   # may be switched off for no-update batch-stat passes
+        self._prep: Dict[Tuple[int, torch.dtype], Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
+        self._arena = None
+        self.embedding_only = False
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(
+                _conv1x1(self.inplanes, planes * block.expansion, stride),
+                nn.BatchNorm2d(planes * block.expansion),
+            )
+        layers = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    # ------------------------------------------------------------------
+    def set_compute_dtype(self, dtype: str) -> "SSIPResNet":
+        self.compute_dtype = _DTYPES[dtype]
+        self._prep.clear()
+        return self
+
+    def blocks(self):
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for b in layer:
+                yield b
+
+    def _apply(self, fn, *args, **kwargs):
+        self._prep.clear()
+        self._arena = None
+        return super()._apply(fn, *args, **kwargs)
+
+    # ------------------------------------------------------------------
+    # flat parameter arena (fused optimizer / bucketed all-reduce)
+    # ------------------------------------------------------------------
+    def flatten_parameters(self):
+        """Re-home every parameter (and its grad) into one contiguous fp32
+        buffer, in ``named_parameters()`` order.  Idempotent."""
+        from .arena import ParamArena
+
+        if self._arena is None or not self._arena.valid():
+            self._arena = ParamArena(list(self.parameters()))
+        return self._arena
+
+    # ------------------------------------------------------------------
+    def forward(self, x):
+        if isinstance(x, DeviceImages):
+            images = x.nhwc4
+            if images.dtype != self.compute_dtype:
+                raise TypeError(f"DeviceImages dtype {images.dtype} != model compute dtype {self.compute_dtype}")
+        else:
+            dev = self.conv1.weight.device
+            if dev.type != "cuda":
+                raise RuntimeError("SSIPResNet runs on the HIP device only; call model.to('cuda') first")
+            x = x.to(dev, non_blocking=True)
+            if x.dim() != 4 or x.shape[1] != 3:
+                raise ValueError(f"expected a [B,3,H,W] batch, got {tuple(x.shape)}")
+            images = ops.nchw_to_nhwc(x, 4, self.compute_dtype)
+        params = [p for p in self.parameters()]
+        return _NetFn.apply(self, images, *params)
+
+
+class _NetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model: SSIPResNet, images: torch.Tensor, *params):
+        train = model.training
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        # note: inside autograd.Function.forward grad mode is disabled; the
+        # decision is taken from the inputs' requires_grad
+        need_grad = any(p.requires_grad for p in params)
+        saved = _forward(model, images, train=train, save=need_grad and train)
+        ctx.model = model
+        ctx.saved = saved
+        out = saved.feat.view(saved.N, -1, 1, 1) if model.embedding_only else saved.logits
+        if model.embedding_only:
+            ctx.mark_non_differentiable(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        model: SSIPResNet = ctx.model
+        saved: _Saved = ctx.saved
+        if saved is None or saved.stem is None or not model.training:
+            raise RuntimeError("ssip: backward requires a train-mode forward with trainable parameters")
+        _backward(model, saved, dlogits.contiguous().float())
+        ctx.saved = None
+        return (None, None) + (None,) * len(list(model.parameters()))
+
+
+# ---------------------------------------------------------------------------
+# forward engine
+# ---------------------------------------------------------------------------
+def _geom(conv: nn.Conv2d, N: int, H: int, W: int) -> ConvGeom:
+    K, C, R, S = conv.weight.shape
+    stem = C == 3
+    return ConvGeom(N=N, H=H, W=W, C=4 if stem else C, K=K, R=R, S=8 if stem else S,
+                    stride=conv.stride[0], pad=conv.padding[0], c_real=C, s_real=S)
+
+
+def _prepped(model: SSIPResNet, conv: nn.Conv2d, g: ConvGeom, need_t: bool):
+    dt = model.compute_dtype
+    key = (id(conv), dt)
+    ent = model._prep.get(key)
+    w = conv.weight
+    if ent is None or (need_t and ent[1] is None):
+        krsc = torch.empty((g.K, g.R, g.S, g.C), device=w.device, dtype=dt)
+        crsk = torch.empty((g.C, g.R, g.S, g.K), device=w.device, dtype=dt) if need_t else None
+        ent = (krsc, crsk)
+        model._prep[key] = ent
+    # weights change every optimizer step: re-prepare every forward (one
+    # HBM-bound pass over 44.7 MB of fp32 masters for ResNet-18)
+    ops.weight_prep(w.detach(), dt, g.C, g.S, ent[0], ent[1] if need_t else None)
+    return ent
+
+
+def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool, save: bool,
+             update_running: bool) -> _ConvRec:
+    g = _geom(conv, N, H, W)
+    dt = model.compute_dtype
+    krsc, _ = _prepped(model, conv, g, need_t=save)
+    y = torch.empty((N, g.P, g.Q, g.K), device=x.device, dtype=dt)
+    stats = torch.empty((4, g.K), device=x.device, dtype=torch.float32)
+    if train:
+        nparts = ops.conv_fwd_partial_floats(g)
+        partial = torch.empty(nparts, device=x.device, dtype=torch.float32)
+        ops.conv_fwd(g, x, krsc, y, partial)
+        ops.bn_finalize(g.K, nparts // (3 * g.K), partial, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                        bn.running_var, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
+                        update_running, stats[0], stats[1], stats[2], stats[3])
+    else:
+        ops.conv_fwd(g, x, krsc, y, None)
+        ops.bn_eval_coeffs(g.K, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.eps,
+                           stats[0], stats[1], stats[2], stats[3])
+    return _ConvRec(geom=g, conv=conv, bn=bn, x=x, y=y, stats=stats)
+
+
+def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool) -> _Saved:
+    N, H, W, C4 = images.shape
+    dt = model.compute_dtype
+    upd = train and model.bn_update_running
+    sv = _Saved(dtype=dt, N=N)
+    dev = images.device
+    # stem: conv 7x7/2 -> BN -> ReLU -> maxpool 3x3/2
+    rec = _conv_bn(model, model.conv1, model.bn1, images, N, H, W, train, save, upd)
+    g = rec.geom
+    z1 = torch.empty_like(rec.y)
+    ops.bn_apply(N * g.P * g.Q, g.K, rec.y, rec.stats[2], rec.stats[3], None, True, z1)
+    rec.z = z1
+    mp = model.maxpool
+    k, s, pd = mp.kernel_size, mp.stride, mp.padding
+    Hp = (g.P + 2 * pd - k) // s + 1
+    Wp = (g.Q + 2 * pd - k) // s + 1
+    pool = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt)
+    idx = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=torch.uint8)
+    ops.maxpool_fwd(N, g.P, g.Q, g.K, k, s, pd, z1, pool, idx)
+    if save:
+        sv.stem, sv.pool_out, sv.pool_idx, sv.pool_hw = rec, pool, idx, (g.P, g.Q)
+    x, Hc, Wc = pool, Hp, Wp
+    for blk in model.blocks():
+        recs = []
+        z = x
+        h, w = Hc, Wc
+        stages = blk.stages()
+        for i, (conv, bn) in enumerate(stages):
+            r = _conv_bn(model, conv, bn, z, N, h, w, train, save, upd)
+            h, w = r.geom.P, r.geom.Q
+            if i < len(stages) - 1:
+                zz = torch.empty_like(r.y)
+                ops.bn_apply(N * h * w, r.geom.K, r.y, r.stats[2], r.stats[3], None, True, zz)
+                r.z = zz
+                z = zz
+            recs.append(r)
+        last = recs[-1]
+        ds = None
+        if blk.downsample is not None:
+            ds = _conv_bn(model, blk.downsample[0], blk.downsample[1], x, N, Hc, Wc, train, save, upd)
+            ident = torch.empty_like(ds.y)
+            ops.bn_apply(N * h * w, ds.geom.K, ds.y, ds.stats[2], ds.stats[3], None, False, ident)
+        else:
+            ident = x
+        out = torch.empty_like(last.y)
+        ops.bn_apply(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], ident, True, out)
+        last.z = out
+        if save:
+            sv.blocks.append((recs, ds, x))
+        x, Hc, Wc = out, h, w
+    C = x.shape[-1]
+    feat = torch.empty((N, C), device=dev, dtype=torch.float32)
+    if model.embedding_only:
+        ops.avgpool_fc_fwd(N, Hc * Wc, C, 0, x, None, None, feat, None)
+        sv.logits = None
+    else:
+        J = model.fc.out_features
+        logits = torch.empty((N, J), device=dev, dtype=torch.float32)
+        ops.avgpool_fc_fwd(N, Hc * Wc, C, J, x, model.fc.weight.detach(), model.fc.bias.detach(), feat, logits)
+        sv.logits = logits
+    sv.feat = feat
+    sv.last, sv.last_pq = x, Hc * Wc
+    if train and upd:
+        _bump_batches_tracked(model)
+    return sv
+
+
+def _bump_batches_tracked(model: SSIPResNet):
+    t = getattr(model, "_nbt", None)
+    if t is None:
+        t = [m.num_batches_tracked for m in model.modules()
+             if isinstance(m, nn.BatchNorm2d) and m.num_batches_tracked is not None]
+        model._nbt = t
+    torch._foreach_add_(t, 1)
+
+
+# ---------------------------------------------------------------------------
+# backward engine
+# ---------------------------------------------------------------------------
+def _grad_target(p: torch.Tensor, arena) -> Tuple[torch.Tensor, bool]:
+    """Tensor to write p's gradient into, and whether to accumulate."""
+    if p.grad is None:
+        if arena is not None and arena.owns(p):
+            p.grad = arena.grad_view(p)
+        else:
+            p.grad = torch.empty_like(p)
+        return p.grad, False
+    return p.grad, True
+
+
+def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
+    dt = sv.dtype
+    N = sv.N
+    arena = model._arena if (model._arena is not None and model._arena.valid()) else None
+    dev = dlogits.device
+    fc = model.fc
+    C = sv.last.shape[-1]
+    J = fc.out_features
+    # which stages need input gradients: anything downstream of the first trainable layer
+    trunk = [model.conv1, model.bn1] + [m for b in model.blocks() for m in b.modules() if m is not b]
+    trunk_trainable = any(p.requires_grad for m in trunk for p in m.parameters(recurse=False))
+    fc_w = fc.weight
+    dw = db = None
+    accw = accb = False
+    if fc_w.requires_grad:
+        dw, accw = _grad_target(fc_w, arena)
+    if fc.bias is not None and fc.bias.requires_grad:
+        db, accb = _grad_target(fc.bias, arena)
+    if not trunk_trainable:
+        if dw is not None:
+            ops.avgpool_fc_bwd(dt, N, sv.last_pq, C, J, dlogits, fc_w.detach(), sv.feat, None, dw,
+                               db, accw)
+        return
+    dz = torch.empty_like(sv.last)
+    if dw is not None and db is not None and accw != accb:
+        raise RuntimeError("ssip: fc weight/bias grads must both be fresh or both accumulate")
+    ops.avgpool_fc_bwd(dt, N, sv.last_pq, C, J, dlogits, fc_w.detach(), sv.feat, dz, dw, db, accw)
+
+    # earliest trainable stage decides where dgrad can stop
+    stage_params = [[model.conv1, model.bn1]] + [[m for m in b.modules() if m is not b] for b in model.blocks()]
+    first_trainable = None
+    for i, mods in enumerate(stage_params):
+        if any(p.requires_grad for m in mods for p in m.parameters(recurse=False)):
+            first_trainable = i
+            break
+
+    ws_bytes = 0
+    for recs, ds, _ in sv.blocks:
+        for r in recs + ([ds] if ds is not None else []):
+            ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(r.geom))
+    ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(sv.stem.geom))
+    workspace = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+    coef_buf = torch.empty(3 * 2048, device=dev, dtype=torch.float32)
+
+    def bn_backward(rec: _ConvRec, dzin, zmask, dpre=None):
+        g = rec.geom
+        M = N * g.P * g.Q
+        bn = rec.bn
+        dgam = dbet = None
+        acc = False
+        if bn.weight.requires_grad:
+            dgam, acc = _grad_target(bn.weight, arena)
+        if bn.bias.requires_grad:
+            dbet, acc2 = _grad_target(bn.bias, arena)
+            if dgam is not None and acc2 != acc:
+                raise RuntimeError("ssip: BN weight/bias grads must both be fresh or both accumulate")
+            acc = acc2
+        dy = torch.empty_like(rec.y)
+        partial = torch.empty(ops.bn_bwd_partial_floats(M, g.K), device=dev, dtype=torch.float32)
+        ops.bn_bwd(M, g.K, dzin, zmask, rec.y, rec.stats[0], rec.stats[1], bn.weight.detach(), dgam, dbet, acc,
+                   dy, dpre, partial, coef_buf[: 3 * g.K])
+        return dy
+
+    def conv_wgrad(rec: _ConvRec, dy):
+        w = rec.conv.weight
+        if not w.requires_grad:
+            return
+        tgt, acc = _grad_target(w, arena)
+        ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
+
+    def conv_dgrad(rec: _ConvRec, dy, out, add=None):
+        _, crsk = _prepped_t(model, rec)
+        ops.conv_dgrad(rec.geom, dy, crsk, out, add)
+
+    nblocks = len(sv.blocks)
+    for bi in range(nblocks - 1, -1, -1):
+        recs, ds, xin = sv.blocks[bi]
+        stage_idx = bi + 1
+        need_dx = first_trainable is not None and first_trainable < stage_idx
+        last = recs[-1]
+        dpre = torch.empty_like(last.y)
+        dy = bn_backward(last, dz, last.z, dpre)
+        dy_ds = None
+        if ds is not None:
+            dy_ds = bn_backward(ds, dpre, None)
+        # main path, last conv back to the first
+        g_cur = dy
+        for i in range(len(recs) - 1, -1, -1):
+            r = recs[i]
+            conv_wgrad(r, g_cur)
+            if i > 0:
+                dzp = torch.empty_like(r.x)
+                conv_dgrad(r, g_cur, dzp)
+                g_cur = bn_backward(recs[i - 1], dzp, recs[i - 1].z)
+            else:
+                if need_dx:
+                    dxin = torch.empty_like(xin)
+                    if ds is None:
+                        conv_dgrad(r, g_cur, dxin, dpre)
+                    else:
+                        conv_dgrad(r, g_cur, dxin)
+                else:
+                    dxin = None
+        if ds is not None:
+            conv_wgrad(ds, dy_ds)
+            if dxin is not None:
+                conv_dgrad(ds, dy_ds, dxin, dxin)
+        dz = dxin
+        if dz is None:
+            return
+    # stem: maxpool backward -> BN/ReLU backward -> conv1 wgrad
+    stem = sv.stem
+    P1, Q1 = sv.pool_hw
+    mp = model.maxpool
+    dz1 = torch.empty_like(stem.y)
+    ops.maxpool_bwd(N, P1, Q1, stem.geom.K, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, dz1)
+    dy1 = bn_backward(stem, dz1, stem.z)
+    conv_wgrad(stem, dy1)
+
+
+def _prepped_t(model: SSIPResNet, rec: _ConvRec):
+    dt = model.compute_dtype
+    ent = model._prep.get((id(rec.conv), dt))
+    if ent is None or ent[1] is None:
+        ent = _prepped(model, rec.conv, rec.geom, need_t=True)
+    return ent
+
+
+# ---------------------------------------------------------------------------
+# factory helpers
+# ---------------------------------------------------------------------------
+def resnet(arch: str = "resnet18", num_classes: int = 1000, dtype: str = "fp32") -> SSIPResNet:
+    return SSIPResNet(arch, num_classes=num_classes, dtype=dtype)
+
+
+def replace_fc(model: SSIPResNet, num_classes: int) -> SSIPResNet:
+    """`model.fc = nn.Linear(in_features, num_classes)` as create_model does
+    (src/training/common.py:299-304) — consumes the torch RNG identically."""
+    model.fc = nn.Linear(model.fc.in_features, num_classes)
+    return model

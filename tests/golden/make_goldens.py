@@ -1,0 +1,196 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE's
+own Python (Septimus4/semi-supervised-image-processing, read-only at
+/root/reference) on CPU in the build container.
+
+torchvision is not installed in this image, so `import torchvision` is
+served by the oracle's restatement (oracle/torchvision_restate/), which
+delegates every image op to Pillow exactly as torchvision does.  Nothing in
+this script runs on the GPU box (it needs /root/reference); the fixtures it
+writes are small data files (inputs and expected outputs).
+
+Run:  python tests/golden/make_goldens.py
+"""
+from __future__ import annotations
+
+import json
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+ROOT = OUT.parents[1]
+
+
+def main() -> None:
+    if not REF.exists():
+        sys.exit("make_goldens: /root/reference not present (fixtures are generated in the build container only)")
+    sys.path.insert(0, str(ROOT / "oracle" / "torchvision_restate"))
+    sys.path.insert(0, str(REF / "src"))
+    sys.path.insert(0, str(REF))
+    import torch
+    from PIL import Image
+    from torch.utils.data import DataLoader, Dataset
+
+    from training import common as C  # reference module
+    from training import semi_supervised as SS  # reference module
+    import src.feature_extraction as FE  # reference module
+
+    data = REF / "mri_dataset_brain_cancer_oc"
+    goldens = {}
+
+    # 1. stratified split on the real labelled set (seed 42 = default; and 7)
+    import torchvision
+
+    base = torchvision.datasets.ImageFolder(data / "avec_labels")
+    targets = list(base.targets)
+    splits = {}
+    for seed in (42, 7):
+        tr, va, te = C.stratified_split(targets, 0.2, 0.2, seed)
+        splits[str(seed)] = {"train": tr.tolist(), "val": va.tolist(), "test": te.tolist()}
+    goldens["splits"] = {"targets": targets, "classes": base.classes,
+                         "samples": [str(Path(p).relative_to(data)) for p, _ in base.samples], "by_seed": splits}
+    # a synthetic, unbalanced case
+    tgt2 = [0] * 30 + [1] * 70
+    tr, va, te = C.stratified_split(tgt2, 0.15, 0.25, 3)
+    goldens["splits"]["synthetic"] = {"targets": tgt2, "val": 0.15, "test": 0.25, "seed": 3,
+                                      "train": tr.tolist(), "val_idx": va.tolist(), "test_idx": te.tolist()}
+
+    # 2. balanced sampler: weights + draws under a fixed seed
+    samp = []
+    for labels, seed in (([0, 1, 1, 1, 0, 1, 1, 1, 1, 0], 5), ([1] * 12, 9), ([0] * 3 + [1] * 9, 11)):
+        s = C.make_balanced_sampler(labels)
+        torch.manual_seed(seed)
+        draws = list(iter(s))
+        samp.append({"labels": labels, "seed": seed, "weights": [float(w) for w in s.weights.tolist()],
+                     "num_samples": s.num_samples, "draws": [int(d) for d in draws]})
+    goldens["sampler"] = samp
+
+    # 3. threshold selection / metrics on seeded probability vectors
+    rng = np.random.default_rng(0)
+    thr = []
+    cases = [
+        (np.array([1, 0, 1, 0, 1]), np.array([0.9, 0.8, 0.7, 0.2, 0.1]), 0.98, 0.6, None, 2.0),
+    ]
+    for i in range(12):
+        n = 20
+        y = rng.integers(0, 2, n)
+        p = np.clip(rng.normal(0.35 + 0.3 * y, 0.2), 0, 1)
+        tr_ = [0.98, 0.9, 0.8, 1.0][i % 4]
+        mp = [None, 0.6, 0.9, 0.99][(i // 4) % 4]
+        mf = [None, 0.3, 0.05][i % 3]
+        cases.append((y, p, tr_, mp, mf, [2.0, 1.0, 0.5][i % 3]))
+    cases.append((np.zeros(6, int), np.linspace(0, 1, 6), 0.9, None, None, 2.0))
+    for y, p, tr_, mp, mf, fb in cases:
+        t, meta = C.select_operating_threshold(y, p, target_recall=tr_, min_precision=mp, max_fpr=mf, f_beta=fb)
+        rec_thr = C.find_threshold_for_target_recall(y, p, tr_)
+        yp = (p >= t).astype(int)
+        conf = C.compute_binary_confusion_metrics(y, yp, 1)
+        acc, f1 = C.compute_accuracy_f1(y.tolist(), yp.tolist())
+        thr.append({"y": y.tolist(), "p": p.tolist(), "target_recall": tr_, "min_precision": mp, "max_fpr": mf,
+                    "f_beta": fb, "threshold": t, "meta": meta, "recall_only_threshold": rec_thr,
+                    "confusion_pos1": conf, "acc": acc, "f1": f1})
+    goldens["thresholds"] = thr
+
+    # 4. transforms on real dataset images (reference build_transforms / build_transform)
+    names = ["avec_labels/cancer/05340cd4-3bb2-459d-9937-bf27d52d8351.jpg",
+             "avec_labels/normal/" + sorted(p.name for p in (data / "avec_labels" / "normal").iterdir())[0],
+             "sans_label/" + sorted(p.name for p in (data / "sans_label").iterdir())[3]]
+    tfs = C.build_transforms(224)
+    ext = FE.build_transform()
+    srcs, train_out, eval_out, ext_out, flips, angles = [], [], [], [], [], []
+    for k, nm in enumerate(names):
+        im = Image.open(data / nm).convert("RGB")
+        srcs.append(np.asarray(im))
+        seed = 100 + k
+        torch.manual_seed(seed)
+        train_out.append(tfs["train"](im).numpy())
+        torch.manual_seed(seed)
+        flips.append(bool(torch.rand(1) < 0.5))
+        angles.append(float(torch.empty(1).uniform_(-10.0, 10.0).item()))
+        eval_out.append(tfs["eval"](im).numpy())
+        with Image.open(data / nm) as im2:  # extraction: no convert('RGB') (all RGB)
+            ext_out.append(ext(im2).numpy())
+    np.savez_compressed(OUT / "transforms.npz", names=np.array(names), src=np.stack(srcs),
+                        flip=np.array(flips), angle=np.array(angles), train_out=np.stack(train_out),
+                        eval_out=np.stack(eval_out), extract_out=np.stack(ext_out))
+
+    # 5. seeded ResNet-18 (create_model(2, pretrained=False) under seed 42):
+    #    logits (eval + train mode) and 512-D embeddings on the transformed images
+    torch.manual_seed(42)
+    model = C.create_model(2, pretrained=False)
+    x = torch.from_numpy(np.stack(eval_out))
+    model.eval()
+    with torch.no_grad():
+        logits_eval = model(x)
+        emb = torch.flatten(torch.nn.Sequential(*list(model.children())[:-1])(x), 1)
+    model.train()
+    with torch.no_grad():
+        logits_train = model(x)
+    np.savez_compressed(OUT / "resnet18_seed42.npz", x=x.numpy(), logits_eval=logits_eval.numpy(),
+                        logits_train=logits_train.numpy(), embeddings=emb.numpy(),
+                        running_mean_bn1=model.bn1.running_mean.numpy(), running_var_bn1=model.bn1.running_var.numpy())
+
+    # 6. train_model trajectory (reference loop, tiny synthetic dataset, 3 epochs)
+    class Tiny(Dataset):
+        def __init__(self, n, seed):
+            g = torch.Generator().manual_seed(seed)
+            self.x = torch.randn(n, 3, 64, 64, generator=g)
+            self.y = torch.tensor([i % 2 for i in range(n)])
+
+        def __len__(self):
+            return len(self.y)
+
+        def __getitem__(self, i):
+            return self.x[i], int(self.y[i])
+
+    torch.manual_seed(42)
+    m2 = C.create_model(2, pretrained=False)
+    tr_ds, va_ds = Tiny(24, 1), Tiny(8, 2)
+    sampler = C.make_balanced_sampler(tr_ds.y.tolist())
+    tl = DataLoader(tr_ds, batch_size=8, sampler=sampler, num_workers=0)
+    vl = DataLoader(va_ds, batch_size=8, shuffle=False, num_workers=0)
+    opt = torch.optim.AdamW((p for p in m2.parameters() if p.requires_grad), lr=1e-4, weight_decay=1e-4)
+    sch = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", patience=2, factor=0.5)
+    with tempfile.TemporaryDirectory() as td:
+        ck = Path(td) / "best.pt"
+        m2, hist = C.train_model(m2, tl, vl, torch.nn.CrossEntropyLoss(), opt, torch.device("cpu"), scheduler=sch,
+                                 num_epochs=3, early_stopping_patience=3, model_path=ck)
+        saved = torch.load(ck, weights_only=True)
+        same = all(torch.equal(saved[k], v) for k, v in m2.state_dict().items())
+    m2.eval()
+    with torch.no_grad():
+        final_logits = m2(va_ds.x).numpy()
+    goldens["train_model"] = {"history": hist, "final_eval_logits": final_logits.tolist(),
+                              "checkpoint_equals_returned": bool(same), "epochs": 3, "batch_size": 8}
+
+    # 7. generate_pseudo_labels on fixed logits (identity "model" over a tiny loader)
+    class LogitModel(torch.nn.Module):
+        def forward(self, z):
+            return z
+
+    g = torch.Generator().manual_seed(3)
+    z = torch.randn(40, 2, generator=g) * 1.5
+    paths = [f"img_{i:03d}.jpg" for i in range(40)]
+    pl_loader = DataLoader(list(zip(z, paths)), batch_size=16, shuffle=False)
+    pseudo = SS.generate_pseudo_labels(LogitModel(), pl_loader, torch.device("cpu"), threshold=0.7)
+    goldens["pseudo_labels"] = {"logits": z.tolist(), "paths": paths, "threshold": 0.7,
+                                "selected": [[p, int(l), float(c)] for p, l, c in pseudo]}
+
+    # 8. feature-extraction host helpers on fixed embeddings
+    e = np.random.default_rng(5).normal(size=(30, 512)).astype(np.float32)
+    recs = [FE.ImageRecord(Path(f"/x/{i}.jpg"), Path(f"sans_label/{i}.jpg"), "unlabeled", None) for i in range(30)]
+    goldens["extraction"] = {"embeddings_seed": 5, "shape": [30, 512], "sanity": FE.run_sanity_checks(e),
+                             "neighbors": FE.nearest_neighbor_probe(e, recs)}
+    recs_ref = FE.discover_image_records(data)
+    goldens["extraction"]["records"] = [[str(r.relative_path), r.bucket, r.label] for r in recs_ref]
+
+    with open(OUT / "goldens.json", "w") as f:
+        json.dump(goldens, f, indent=1, default=float)
+    print("wrote", sorted(p.name for p in OUT.iterdir()))
+
+
+if __name__ == "__main__":
+    main()

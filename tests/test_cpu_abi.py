@@ -1,0 +1,30 @@
+"""CPU: the C-ABI library loads and exports every symbol include/ssip.h
+declares (no compute calls without a GPU)."""
+import re
+from pathlib import Path
+
+from ssip import _lib
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_header_and_binding_agree():
+    hdr = (ROOT / "include" / "ssip.h").read_text()
+    declared = set(re.findall(r"^\s*(?:const char\*|int64_t|int)\s+(ssip_\w+)\(", hdr, re.M))
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    lib = _lib.lib()
+    for name in _lib.EXPORTED_SYMBOLS:
+        assert hasattr(lib, name), name
+    assert lib.ssip_version() == 1
+
+
+def test_argument_errors_surface_as_status_codes():
+    lib = _lib.lib()
+    d = _lib.ConvDesc(1, 8, 8, 24, 64, 3, 3, 1, 1, 8, 8)  # C=24 is not a multiple of 32
+    assert lib.ssip_conv_fwd_partial_floats(d) < 0
+    rc = lib.ssip_conv_fwd(d, 0, None, None, None, None, None)
+    assert rc == -1
+    assert b"multiple of 32" in lib.ssip_last_error()

@@ -1,0 +1,128 @@
+"""GPU parity: implicit-GEMM conv fwd / dgrad / wgrad and BN statistics vs
+torch CPU float64 (the oracle for a floating-point kernel).
+Tolerances: f32 path rel-err <= 2e-5 of max|ref|; bf16 path compares against
+the f64 result on bf16-rounded operands, rel-err <= 1e-2 (output rounding)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ssip import ops
+from ssip.ops import ConvGeom
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    # N, C, H, W, K, R, stride, pad
+    (2, 64, 16, 16, 64, 3, 1, 1),
+    (2, 64, 16, 16, 128, 3, 2, 1),
+    (2, 128, 15, 15, 256, 1, 2, 0),
+    (3, 32, 7, 7, 96, 3, 1, 1),
+    (2, 3, 32, 32, 64, 7, 2, 3),   # stem (C padded to 4, S to 8)
+    (1, 256, 7, 7, 512, 3, 1, 1),
+]
+
+
+def _geom(N, C, H, W, K, R, st, pd):
+    stem = C == 3
+    return ConvGeom(N=N, H=H, W=W, C=4 if stem else C, K=K, R=R, S=8 if stem else R, stride=st, pad=pd,
+                    c_real=C, s_real=R)
+
+
+def _to_nhwc(x, Cp, dt, dev):
+    return ops.nchw_to_nhwc(x.to(dev), Cp, dt)
+
+
+def _relerr(a, b):
+    return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_conv_fwd(dev, shape, dtname):
+    torch.manual_seed(0)
+    N, C, H, W, K, R, st, pd = shape
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    g = _geom(*shape)
+    x = torch.randn(N, C, H, W)
+    w = torch.randn(K, C, R, R) * 0.1
+    if dt == torch.bfloat16:
+        x = x.bfloat16().float()
+        w = w.bfloat16().float()
+    ref = F.conv2d(x.double(), w.double(), stride=st, padding=pd).permute(0, 2, 3, 1)
+    xh = _to_nhwc(x, g.C, dt, dev)
+    krsc = torch.empty((K, R, g.S, g.C), device=dev, dtype=dt)
+    ops.weight_prep(w.to(dev), dt, g.C, g.S, krsc, None)
+    y = torch.empty((N, g.P, g.Q, K), device=dev, dtype=dt)
+    part = torch.empty(ops.conv_fwd_partial_floats(g), device=dev)
+    ops.conv_fwd(g, xh, krsc, y, part)
+    torch.cuda.synchronize()
+    assert y.shape[1:3] == ref.shape[1:3]
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    assert _relerr(y.cpu(), ref) < tol
+    # BN statistics from the partials
+    stats = torch.empty((4, K), device=dev)
+    gamma = torch.ones(K, device=dev)
+    beta = torch.zeros(K, device=dev)
+    rm = torch.zeros(K, device=dev)
+    rv = torch.ones(K, device=dev)
+    ops.bn_finalize(K, part.numel() // (3 * K), part, gamma, beta, rm, rv, 0.1, 1e-5, True, stats[0], stats[1],
+                    stats[2], stats[3])
+    torch.cuda.synchronize()
+    r = ref.reshape(-1, K)
+    mean = r.mean(0)
+    var = r.var(0, unbiased=False)
+    tol_s = 1e-5 if dt == torch.float32 else 1e-2
+    assert _relerr(stats[0].cpu(), mean) < tol_s * 10
+    assert _relerr((1 / stats[1].cpu().double() ** 2 - 1e-5), var) < tol_s * 10
+    assert _relerr(rv.cpu(), 0.9 + 0.1 * r.var(0, unbiased=True)) < tol_s * 10
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3])
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_conv_dgrad(dev, shape, dtname):
+    torch.manual_seed(1)
+    N, C, H, W, K, R, st, pd = shape
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    g = _geom(*shape)
+    w = torch.randn(K, C, R, R) * 0.1
+    dy = torch.randn(N, K, g.P, g.Q)
+    add = torch.randn(N, C, H, W)
+    if dt == torch.bfloat16:
+        w, dy, add = w.bfloat16().float(), dy.bfloat16().float(), add.bfloat16().float()
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.double(), dy.double(), stride=st, padding=pd)
+    ref = (ref + add.double()).permute(0, 2, 3, 1)
+    crsk = torch.empty((C, R, R, K), device=dev, dtype=dt)
+    ops.weight_prep(w.to(dev), dt, C, R, None, crsk)
+    dyh = _to_nhwc(dy, K, dt, dev)
+    addh = _to_nhwc(add, C, dt, dev)
+    dx = torch.empty((N, H, W, C), device=dev, dtype=dt)
+    ops.conv_dgrad(g, dyh, crsk, dx, addh)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    assert _relerr(dx.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_conv_wgrad(dev, shape, dtname):
+    torch.manual_seed(2)
+    N, C, H, W, K, R, st, pd = shape
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    g = _geom(*shape)
+    x = torch.randn(N, C, H, W)
+    dy = torch.randn(N, K, g.P, g.Q)
+    if dt == torch.bfloat16:
+        x, dy = x.bfloat16().float(), dy.bfloat16().float()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, R, R), dy.double(), stride=st, padding=pd)
+    xh = _to_nhwc(x, g.C, dt, dev)
+    dyh = _to_nhwc(dy, K, dt, dev)
+    dw = torch.full((K, C, R, R), 7.0, device=dev)
+    ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
+    ops.conv_wgrad(g, dyh, xh, dw, False, ws)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dt == torch.float32 else 1e-4
+    assert _relerr(dw.cpu(), ref) < tol
+    # accumulate mode adds on top
+    ops.conv_wgrad(g, dyh, xh, dw, True, ws)
+    torch.cuda.synchronize()
+    assert _relerr(dw.cpu(), 2 * ref) < tol

@@ -1,0 +1,206 @@
+"""GPU parity of the non-GEMM kernels vs torch CPU float64 autograd:
+BatchNorm train forward/backward (+ReLU, +residual), max-pool, global
+average pool + fc, cross-entropy, pseudo-label selection, consistency loss,
+AdamW.  Tolerances: f32 rel-max 1e-5 (1e-4 for reductions over >1e4
+elements), bf16 rel-max 2e-2; max-pool indices and pseudo-label picks exact."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ssip import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_train_fwd_bwd(dev, dtname, relu, res):
+    torch.manual_seed(0)
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    N, C, H, W = 4, 64, 10, 10
+    y = (torch.randn(N, C, H, W) * 2 + 0.5)
+    r = torch.randn(N, C, H, W)
+    g = torch.randn(N, C, H, W)
+    gamma = torch.rand(C) + 0.5
+    beta = torch.randn(C) * 0.1
+    if dt == torch.bfloat16:
+        y, r, g = y.bfloat16().float(), r.bfloat16().float(), g.bfloat16().float()
+    yd = y.double().requires_grad_()
+    gd = gamma.double().requires_grad_()
+    bd = beta.double().requires_grad_()
+    out = F.batch_norm(yd, None, None, gd, bd, training=True, eps=1e-5)
+    if res:
+        out = out + r.double()
+    if relu:
+        out = torch.relu(out)
+    out.backward(g.double())
+    # device path: stats from a fake single-tile partial set computed on the host
+    M = N * H * W
+    ym = _nhwc(y).reshape(M, C)
+    part = torch.stack([torch.full((C,), float(M)), ym.double().sum(0).float(),
+                        ((ym.double() - ym.double().mean(0)) ** 2).sum(0).float()], 1)  # [C][3] (1 tile)
+    part = part.reshape(C, 1, 3).contiguous().to(dev)
+    stats = torch.empty(4, C, device=dev)
+    rm = torch.zeros(C, device=dev)
+    rv = torch.ones(C, device=dev)
+    ops.bn_finalize(C, 1, part, gamma.to(dev), beta.to(dev), rm, rv, 0.1, 1e-5, True, stats[0], stats[1], stats[2],
+                    stats[3])
+    yh = _nhwc(y).to(dev, dt)
+    rh = _nhwc(r).to(dev, dt) if res else None
+    z = torch.empty_like(yh)
+    ops.bn_apply(M, C, yh, stats[2], stats[3], rh, relu, z)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    assert _rel(z.cpu(), _nhwc(out.detach())) < tol
+    gh = _nhwc(g).to(dev, dt)
+    dgam = torch.empty(C, device=dev)
+    dbet = torch.empty(C, device=dev)
+    dy = torch.empty_like(yh)
+    dpre = torch.empty_like(yh)
+    part_b = torch.empty(ops.bn_bwd_partial_floats(M, C), device=dev)
+    coef = torch.empty(3 * C, device=dev)
+    ops.bn_bwd(M, C, gh, z if relu else None, yh, stats[0], stats[1], gamma.to(dev), dgam, dbet, False, dy, dpre,
+               part_b, coef)
+    torch.cuda.synchronize()
+    tolb = 1e-4 if dt == torch.float32 else 5e-2
+    assert _rel(dgam, gd.grad) < tolb
+    assert _rel(dbet, bd.grad) < tolb
+    assert _rel(dy.cpu(), _nhwc(yd.grad)) < tolb
+    if relu:
+        mask = (_nhwc(out.detach()) > 0)
+        assert _rel(dpre.cpu(), _nhwc(g) * mask) < tol
+    # accumulate mode
+    ops.bn_bwd(M, C, gh, z if relu else None, yh, stats[0], stats[1], gamma.to(dev), dgam, dbet, True, dy, None,
+               part_b, coef)
+    torch.cuda.synchronize()
+    assert _rel(dgam, 2 * gd.grad) < tolb
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_maxpool(dev, dtname):
+    torch.manual_seed(0)
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    N, C, H, W = 2, 64, 17, 16
+    x = torch.relu(torch.randn(N, C, H, W))  # many ties at 0, like the stem
+    x = x.to(dt).float()
+    xd = x.double().requires_grad_()
+    y = F.max_pool2d(xd, 3, 2, 1)
+    g = torch.randn_like(y).to(dt).double()
+    y.backward(g)
+    xh = _nhwc(x).to(dev, dt)
+    P, Q = y.shape[2], y.shape[3]
+    yh = torch.empty(N, P, Q, C, device=dev, dtype=dt)
+    idx = torch.empty(N, P, Q, C, device=dev, dtype=torch.uint8)
+    ops.maxpool_fwd(N, H, W, C, 3, 2, 1, xh, yh, idx)
+    dx = torch.empty_like(xh)
+    ops.maxpool_bwd(N, H, W, C, 3, 2, 1, _nhwc(g.float()).to(dev, dt), idx, dx)
+    torch.cuda.synchronize()
+    assert torch.equal(yh.cpu().float(), _nhwc(y.detach()).float())
+    tol = 1e-6 if dt == torch.float32 else 1e-2
+    assert _rel(dx.cpu(), _nhwc(xd.grad)) < tol
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_avgpool_fc(dev, dtname):
+    torch.manual_seed(0)
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    B, C, H, W, J = 5, 512, 7, 7, 2
+    z = torch.randn(B, C, H, W).to(dt).float()
+    w = torch.randn(J, C) * 0.05
+    b = torch.randn(J)
+    zd = z.double().requires_grad_()
+    wd = w.double().requires_grad_()
+    bd = b.double().requires_grad_()
+    feat = zd.mean((2, 3))
+    logits = feat @ wd.t() + bd
+    gl = torch.randn(B, J).double()
+    logits.backward(gl)
+    zh = _nhwc(z).to(dev, dt)
+    f = torch.empty(B, C, device=dev)
+    lo = torch.empty(B, J, device=dev)
+    ops.avgpool_fc_fwd(B, H * W, C, J, zh, w.to(dev), b.to(dev), f, lo)
+    dz = torch.empty_like(zh)
+    dw = torch.empty(J, C, device=dev)
+    db = torch.empty(J, device=dev)
+    ops.avgpool_fc_bwd(dt, B, H * W, C, J, gl.float().to(dev), w.to(dev), f, dz, dw, db, False)
+    torch.cuda.synchronize()
+    assert _rel(f, feat) < 1e-5
+    assert _rel(lo, logits) < 1e-5
+    assert _rel(dw, wd.grad) < 1e-5
+    assert _rel(db, bd.grad) < 1e-5
+    assert _rel(dz.cpu(), _nhwc(zd.grad)) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+def test_cross_entropy_and_select(dev):
+    torch.manual_seed(0)
+    z = torch.randn(300, 2) * 3
+    y = torch.randint(0, 2, (300,))
+    zd = z.double().requires_grad_()
+    loss = F.cross_entropy(zd, y)
+    loss.backward()
+    l, dl, pred = ops.cross_entropy(z.to(dev), y.to(dev))
+    torch.cuda.synchronize()
+    assert abs(l.item() - loss.item()) < 1e-5 * max(1.0, abs(loss.item()))
+    assert _rel(dl, zd.grad) < 1e-5
+    assert torch.equal(pred.cpu(), z.argmax(1))
+    probs, conf, p2, keep, pos = ops.softmax_select(z.to(dev), 0.7, 0)
+    torch.cuda.synchronize()
+    pr = torch.softmax(z, 1)
+    c, a = pr.max(1)
+    assert _rel(probs, pr) < 1e-6
+    assert torch.equal(p2.cpu(), a)
+    assert torch.equal(keep.cpu().bool(), c >= 0.7)
+    assert _rel(pos, pr[:, 0]) < 1e-6
+
+
+def test_semi_loss(dev):
+    torch.manual_seed(1)
+    zl = torch.randn(16, 2)
+    yl = torch.randint(0, 2, (16,))
+    zw = torch.randn(24, 2) * 2
+    zs = torch.randn(24, 2)
+    tau, lam = 0.7, 1.0
+    zld = zl.double().requires_grad_()
+    zsd = zs.double().requires_grad_()
+    pw = torch.softmax(zw.double(), 1)
+    conf, pseudo = pw.max(1)
+    mask = (conf >= tau).double()
+    lu = (F.cross_entropy(zsd, pseudo, reduction="none") * mask).mean()
+    ll = F.cross_entropy(zld, yl)
+    tot = ll + lam * lu
+    tot.backward()
+    out, dzl, dzs, ps, mk = ops.semi_loss(zl.to(dev), yl.to(dev), zw.to(dev), zs.to(dev), tau, lam)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    assert abs(o[0].item() - tot.item()) < 1e-5
+    assert abs(o[3].item() - mask.sum().item()) < 0.5
+    assert torch.equal(ps.cpu(), pseudo)
+    assert _rel(dzl, zld.grad) < 1e-5
+    assert _rel(dzs, zsd.grad) < 1e-5
+
+
+def test_adamw_matches_torch(dev):
+    torch.manual_seed(0)
+    p0 = torch.randn(1000)
+    grads = [torch.randn(1000) for _ in range(3)]
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
+    p = p0.clone().to(dev)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for t, g in enumerate(grads, 1):
+        ref.grad = g.clone()
+        opt.step()
+        ops.adamw(p, g.to(dev), m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-2, t)
+    torch.cuda.synchronize()
+    assert _rel(p, ref.detach()) < 1e-6

@@ -55,8 +55,9 @@ int ssip_version(void);
 
 /* ------------------------------------------------------------------------
  * Convolution as implicit GEMM on MFMA (torchvision nn.Conv2d, bias=False).
- * x: [N][H][W][C], y/dy: [N][P][Q][K].  C must be a multiple of 32, or C == 4
- * with S == 8 (the padded 7x7 stem: channel 3 and filter column 7 are zero).
+ * x: [N][H][W][C], y/dy: [N][P][Q][K].  C and K must be multiples of 64
+ * (bf16) / 32 (f32), or C == 4 with S == 8 (the padded 7x7 stem: channel 3
+ * and filter column 7 are zero).
  * ---------------------------------------------------------------------- */
 typedef struct ssip_conv_desc {
   int N, H, W, C; /* input (C = stored channels)          */
@@ -68,8 +69,10 @@ typedef struct ssip_conv_desc {
 
 /* floats needed for the BatchNorm partial-statistics buffer of ssip_conv_fwd */
 int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d);
+/* number of M-tiles (records per channel) ssip_conv_fwd writes for this dtype */
+int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype);
 /* y = conv(x, w); w_krsc: [K][R][S][C] in dtype.  bn_partial (nullable):
- * fp32 {count, sum, M2} per (M-tile, channel) consumed by ssip_bn_finalize. */
+ * fp32 {count, sum, M2} per (channel, M-tile) consumed by ssip_bn_finalize. */
 int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, void* y, float* bn_partial,
                   void* stream);
 /* dx = conv_transpose(dy, w) (+ dx_add, nullable); w_crsk: [C][R][S][K] */

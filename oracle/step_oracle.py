@@ -1,0 +1,107 @@
+"""ORACLE (test infrastructure / CPU baseline only): the semi-supervised
+train step restated on the CPU in plain torch fp32 — the same algorithm as
+ssip.semi_step.SemiStep, with the reference's own pieces:
+
+  views     torchvision train transform on PIL images (Resize -> flip ->
+            rotate -> ToTensor -> Normalize, src/training/common.py:96-119),
+            strong view = the same ops with a +-30 deg rotation plus
+            brightness/contrast jitter and a cutout square
+  model     torchvision resnet18 (restated in oracle/torchvision_restate)
+  loss      nn.CrossEntropyLoss (src/training/semi_supervised.py:111) on the
+            labelled half + masked CE on the strong view with pseudo-labels
+            softmax/max/>=tau (semi_supervised.py:57-66)
+  optimizer torch.optim.AdamW(lr=1e-4, wd=1e-4)
+
+Used by bench.py's `cpu_baseline` leg (timed on the GPU box's host cores).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from PIL import Image
+
+from .torchvision_restate.torchvision import models as tvm
+from .torchvision_restate.torchvision import transforms as T
+
+MEAN = [0.485, 0.456, 0.406]
+STD = [0.229, 0.224, 0.225]
+
+
+def _view(img: Image.Image, size: int, degrees: float, strong: bool, g: torch.Generator) -> torch.Tensor:
+    img = img.resize((size, size), Image.BILINEAR) if img.size != (size, size) else img
+    if torch.rand(1, generator=g) < 0.5:
+        img = img.transpose(Image.FLIP_LEFT_RIGHT)
+    ang = float(torch.empty(1).uniform_(-degrees, degrees, generator=g).item())
+    img = img.rotate(ang, Image.NEAREST, expand=False, fillcolor=(0, 0, 0))
+    t = T.ToTensor()(img)
+    if strong:
+        u = torch.rand(4, generator=g)
+        b = 1.0 + 0.4 * (2 * float(u[0]) - 1)
+        c = 1.0 + 0.4 * (2 * float(u[1]) - 1)
+        t = ((t * b - 0.5) * c + 0.5).clamp(0, 1)
+        side = int(0.25 * size)
+        x0 = int(float(u[2]) * (size - side))
+        y0 = int(float(u[3]) * (size - side))
+        t[:, y0:y0 + side, x0:x0 + side] = 0.5
+    return T.Normalize(MEAN, STD)(t)
+
+
+class CpuSemiStep:
+    def __init__(self, seed: int = 42, tau: float = 0.7, lambda_u: float = 1.0, size: int = 224):
+        torch.manual_seed(seed)
+        self.model = tvm.resnet18()
+        self.model.fc = torch.nn.Linear(512, 2)
+        self.opt = torch.optim.AdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-4)
+        self.tau, self.lambda_u, self.size = tau, lambda_u, size
+        self.g = torch.Generator().manual_seed(seed)
+
+    def __call__(self, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.ndarray) -> float:
+        S = self.size
+        il = [Image.fromarray(a) for a in x_l]
+        iu = [Image.fromarray(a) for a in x_u]
+        xl = torch.stack([_view(i, S, 10.0, False, self.g) for i in il])
+        xw = torch.stack([_view(i, S, 10.0, False, self.g) for i in iu])
+        xs = torch.stack([_view(i, S, 30.0, True, self.g) for i in iu])
+        m = self.model
+        m.train()
+        with torch.no_grad():
+            # weak view: batch statistics without touching the running stats
+            saved = [(b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone())
+                     for b in m.modules() if isinstance(b, torch.nn.BatchNorm2d)]
+            zw = m(xw)
+            for b, (rm, rv, nb) in zip([b for b in m.modules() if isinstance(b, torch.nn.BatchNorm2d)], saved):
+                b.running_mean.copy_(rm)
+                b.running_var.copy_(rv)
+                b.num_batches_tracked.copy_(nb)
+        conf, pseudo = torch.softmax(zw, 1).max(1)
+        mask = (conf >= self.tau).float()
+        self.opt.zero_grad(set_to_none=True)
+        z = m(torch.cat([xl, xs], 0))
+        Bl = xl.shape[0]
+        loss = F.cross_entropy(z[:Bl], y_l) + self.lambda_u * (
+            F.cross_entropy(z[Bl:], pseudo, reduction="none") * mask).mean()
+        loss.backward()
+        self.opt.step()
+        return float(loss)
+
+
+def time_cpu_step(Bl: int = 8, Bu: int = 8, steps: int = 3, threads: int = 16, seed: int = 0) -> Dict:
+    """Images/sec of the CPU step on a bounded sample (steps x (Bl+Bu) images)."""
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(seed)
+    x_l = rng.integers(0, 256, (Bl, 224, 224, 3), dtype=np.uint8)
+    x_u = rng.integers(0, 256, (Bu, 224, 224, 3), dtype=np.uint8)
+    y_l = torch.from_numpy(rng.integers(0, 2, Bl))
+    step = CpuSemiStep()
+    step(x_l, y_l, x_u)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(x_l, y_l, x_u)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": (Bl + Bu) / dt, "step_s": dt, "threads": torch.get_num_threads(),
+            "sample": f"{steps} steps x ({Bl} labelled + {Bu} unlabelled) 224x224 uint8 images, "
+                      f"PIL views + torch fp32 ResNet-18 fwd/bwd + AdamW"}

@@ -8,13 +8,20 @@
 //   FWD   : Y[m=(n,p,q)][k]        = sum_{(r,s,c)} X[n,p*st-pd+r,q*st-pd+s,c] * W[k][r][s][c]
 //   DGRAD : dX[m=(n,h,w)][c]       = sum_{(r,s,k)} dY[n,(h+pd-r)/st,(w+pd-s)/st,k] * WT[c][r][s][k]
 //   WGRAD : dW[k][(r,s,c)]         = sum_{m=(n,p,q)} dY[m][k] * X[n,p*st-pd+r,q*st-pd+s,c]
-// FWD/DGRAD stage A/B as [rows][32] k-contiguous LDS tiles (16-B slot XOR
-// swizzle); WGRAD stages both operands m-major ([32][cols], as they lie in
-// HBM) and reads fragments with ds_read_b64_tr_b16 (bf16) — no register
-// transposes.  bf16 uses v_mfma_f32_16x16x32_bf16; the f32 parity path uses
-// v_mfma_f32_16x16x4_f32 on the same tiles (8 MFMAs per 32-deep k step).
 //
-// FWD also emits per-(M-tile, channel) BatchNorm partial statistics
+// Block = WMW x WNW waves (64-wide), tile BM x BN, k-step BK = 128 bytes of
+// reduction per row (64 bf16 / 32 f32).  FWD/DGRAD stage A/B as
+// [rows][128 B] k-contiguous LDS tiles (16-B slot XOR swizzle, conflict-free
+// ds_read_b128 fragment reads); WGRAD stages both operands m-major
+// ([BK][cols], as they lie in HBM) and reads fragments with
+// ds_read_b64_tr_b16 (bf16) — no register transposes.  Global->LDS staging
+// is register double-buffered (issue k+1 loads before the MFMAs of k, write
+// them to the other LDS buffer after), one barrier per k-step.
+// bf16: v_mfma_f32_16x16x32_bf16; f32 parity path: v_mfma_f32_16x16x4_f32 on
+// the same tiles.  Epilogue goes through LDS so global stores (and the
+// residual-gradient add of DGRAD) are 16-B per lane, row-contiguous.
+//
+// FWD also emits per-(channel, M-tile) BatchNorm partial statistics
 // {count, sum, M2-about-tile-mean} from the fp32 accumulators so the BN
 // batch statistics need no extra pass over Y.  WGRAD is split over the m
 // reduction into fp32 slabs that a second kernel sums in fixed order
@@ -59,25 +66,20 @@ struct ConvArgs {
   float* partial;
 };
 
+template <typename T> struct Traits;
+template <> struct Traits<__bf16> { static constexpr int BK = 64; };
+template <> struct Traits<float> { static constexpr int BK = 32; };
+
 // ---------------------------------------------------------------------------
 // LDS addressing
 // ---------------------------------------------------------------------------
-// FWD/DGRAD tiles: [rows][32 elems].  bf16 rows are 64 B (4 x 16-B slots);
-// slot' = slot ^ g(row) keeps every ds_read_b128 lane group conflict-free.
-template <typename T> struct KTile;
-template <> struct KTile<__bf16> {
-  static constexpr int ROW_BYTES = 64;
-  __device__ static __forceinline__ int off(int row, int slot) {
-    const int g = (0x1320 >> (((row >> 2) & 3) * 4)) & 3;  // [0,2,3,1][(row>>2)&3]
-    return row * 64 + ((slot ^ g) << 4);
-  }
-};
-template <> struct KTile<float> {
-  static constexpr int ROW_BYTES = 144;  // 128 B + 16 B pad
-  __device__ static __forceinline__ int off(int row, int slot) { return row * 144 + (slot << 4); }
-};
+// FWD/DGRAD tiles: [rows][128 B] (8 x 16-B slots).  slot' = slot ^ ((row>>1)&7)
+// makes every 16-lane group of a ds_read_b128 fragment read (rows l&15,
+// slot 4h + (l>>4) for bf16; slots 2(l>>4)+{0,1} for f32) hit 16 distinct
+// 16-B bank slots.
+__device__ __forceinline__ int ktile_off(int row, int slot) { return row * 128 + ((slot ^ ((row >> 1) & 7)) << 4); }
 
-// WGRAD tiles: [32 m-rows][COLS elems], cols contiguous (as in HBM).
+// WGRAD tiles: [BK m-rows][COLS elems], cols contiguous (as in HBM).
 template <typename T, int COLS> struct MTile;
 template <int COLS> struct MTile<__bf16, COLS> {
   static constexpr int ROW_BYTES = COLS * 2;
@@ -86,8 +88,7 @@ template <int COLS> struct MTile<__bf16, COLS> {
     int h = (row & 3) | (((row >> 3) & 1) << 2);
     return (h * 4) & (UNITS - 1) & ~3;
   }
-  // byte offset of element `col` (multiple of 4) in row
-  __device__ static __forceinline__ int off(int row, int col) {
+  __device__ static __forceinline__ int off(int row, int col) {  // col multiple of 4
     return row * ROW_BYTES + ((((col >> 2) ^ swz(row))) << 3);
   }
 };
@@ -97,7 +98,7 @@ template <int COLS> struct MTile<float, COLS> {
 };
 
 // ---------------------------------------------------------------------------
-// MFMA step over one 32-deep k slice for a FMxFN grid of 16x16 blocks
+// fragments and MFMA
 // ---------------------------------------------------------------------------
 template <typename T> struct Frag;
 template <> struct Frag<__bf16> { bf16x8 v; };
@@ -111,23 +112,24 @@ __device__ __forceinline__ void mma(f32x4& acc, const Frag<float>& a, const Frag
   for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[e], b.v[e], acc, 0, 0, 0);
 }
 
-// k-contiguous fragment: lane holds rows (l&15), k = 8*(l>>4) .. +7
-__device__ __forceinline__ void read_kfrag(Frag<__bf16>& f, const char* base, int row, int kq) {
-  f.v = *reinterpret_cast<const bf16x8*>(base + KTile<__bf16>::off(row, kq));
+// k-contiguous fragment for 32-deep sub-step h: lane holds row (l&15), k = 32h + 8(l>>4) .. +7
+__device__ __forceinline__ void read_kfrag(Frag<__bf16>& f, const char* base, int row, int kq, int h) {
+  f.v = *reinterpret_cast<const bf16x8*>(base + ktile_off(row, 4 * h + kq));
 }
-__device__ __forceinline__ void read_kfrag(Frag<float>& f, const char* base, int row, int kq) {
-  const f32x4 lo = *reinterpret_cast<const f32x4*>(base + KTile<float>::off(row, 2 * kq));
-  const f32x4 hi = *reinterpret_cast<const f32x4*>(base + KTile<float>::off(row, 2 * kq + 1));
+__device__ __forceinline__ void read_kfrag(Frag<float>& f, const char* base, int row, int kq, int) {
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(base + ktile_off(row, 2 * kq));
+  const f32x4 hi = *reinterpret_cast<const f32x4*>(base + ktile_off(row, 2 * kq + 1));
   f.v[0] = lo[0]; f.v[1] = lo[1]; f.v[2] = lo[2]; f.v[3] = lo[3];
   f.v[4] = hi[0]; f.v[5] = hi[1]; f.v[6] = hi[2]; f.v[7] = hi[3];
 }
 
-// m-major fragment (WGRAD): lane l gets column col0 + (l&15), m = 8*(l>>4) .. +7
+// m-major fragment (WGRAD) for sub-step h: lane l gets column col0 + (l&15),
+// m = 32h + 8(l>>4) .. +7
 template <int COLS>
-__device__ __forceinline__ void read_mfrag(Frag<__bf16>& f, const char* base, int col0, int lane) {
+__device__ __forceinline__ void read_mfrag(Frag<__bf16>& f, const char* base, int col0, int lane, int h) {
   typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int r0 = 8 * g + q;
+  const int r0 = 32 * h + 8 * g + q;
   const char* a0 = base + MTile<__bf16, COLS>::off(r0, col0 + 4 * p);
   const char* a1 = base + MTile<__bf16, COLS>::off(r0 + 4, col0 + 4 * p);
   v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a0));
@@ -135,29 +137,18 @@ __device__ __forceinline__ void read_mfrag(Frag<__bf16>& f, const char* base, in
   f.v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 template <int COLS>
-__device__ __forceinline__ void read_mfrag(Frag<float>& f, const char* base, int col0, int lane) {
+__device__ __forceinline__ void read_mfrag(Frag<float>& f, const char* base, int col0, int lane, int h) {
   const int g = lane >> 4, col = col0 + (lane & 15);
 #pragma unroll
   for (int j = 0; j < 8; ++j)
-    f.v[j] = *reinterpret_cast<const float*>(base + MTile<float, COLS>::off(8 * g + j, col));
+    f.v[j] = *reinterpret_cast<const float*>(base + MTile<float, COLS>::off(32 * h + 8 * g + j, col));
 }
-
-// 4-element (one padded pixel) vector load helpers for the conv1 layout (C == 4)
-template <typename T> struct Vec4;
-template <> struct Vec4<__bf16> {
-  typedef __attribute__((ext_vector_type(2))) int raw;
-  raw v;
-};
-template <> struct Vec4<float> {
-  typedef i32x4 raw;
-  raw v;
-};
 
 template <typename T>
 __device__ __forceinline__ void load_v8(Vec8<T>& d, const T* p, bool ok) {
   if (ok) d.load(p); else d.zero();
 }
-// two pixels of 4 channels each
+// two padded pixels of 4 channels each (stem layout)
 template <typename T>
 __device__ __forceinline__ void load_2px(Vec8<T>& d, const T* p0, bool ok0, const T* p1, bool ok1);
 template <>
@@ -173,19 +164,14 @@ __device__ __forceinline__ void load_2px<float>(Vec8<float>& d, const float* p0,
   d.v1 = ok1 ? *reinterpret_cast<const i32x4*>(p1) : (i32x4){0, 0, 0, 0};
 }
 
-template <typename T>
-__device__ __forceinline__ void store_kchunk(char* base, int row, int kc, const Vec8<T>& v);
-template <>
-__device__ __forceinline__ void store_kchunk<__bf16>(char* base, int row, int kc, const Vec8<__bf16>& v) {
-  *reinterpret_cast<i32x4*>(base + KTile<__bf16>::off(row, kc)) = v.v;
+// 8-element chunk kc (0..KC-1) of a k-tile row
+__device__ __forceinline__ void store_kchunk(char* base, int row, int kc, const Vec8<__bf16>& v) {
+  *reinterpret_cast<i32x4*>(base + ktile_off(row, kc)) = v.v;
 }
-template <>
-__device__ __forceinline__ void store_kchunk<float>(char* base, int row, int kc, const Vec8<float>& v) {
-  *reinterpret_cast<i32x4*>(base + KTile<float>::off(row, 2 * kc)) = v.v0;
-  *reinterpret_cast<i32x4*>(base + KTile<float>::off(row, 2 * kc + 1)) = v.v1;
+__device__ __forceinline__ void store_kchunk(char* base, int row, int kc, const Vec8<float>& v) {
+  *reinterpret_cast<i32x4*>(base + ktile_off(row, 2 * kc)) = v.v0;
+  *reinterpret_cast<i32x4*>(base + ktile_off(row, 2 * kc + 1)) = v.v1;
 }
-template <typename T, int COLS>
-__device__ __forceinline__ void store_mchunk(char* base, int row, int col, const Vec8<T>& v);
 template <int COLS>
 __device__ __forceinline__ void store_mchunk(char* base, int row, int col, const Vec8<__bf16>& v) {
   *reinterpret_cast<i32x4*>(base + MTile<__bf16, COLS>::off(row, col)) = v.v;
@@ -196,25 +182,39 @@ __device__ __forceinline__ void store_mchunk(char* base, int row, int col, const
   *reinterpret_cast<i32x4*>(base + MTile<float, COLS>::off(row, col + 4)) = v.v1;
 }
 
+template <int MODE, typename T, int BM, int BN>
+struct Smem {
+  static constexpr int BK = Traits<T>::BK;
+  static constexpr bool WG = (MODE == MODE_WGRAD);
+  static constexpr int A_BYTES = WG ? BK * MTile<T, BM>::ROW_BYTES : BM * 128;
+  static constexpr int B_BYTES = WG ? BK * MTile<T, BN>::ROW_BYTES : BN * 128;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int EPI = WG ? 0 : BM * (BN * (int)sizeof(T) + 16);
+  static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+};
+
 // ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
-template <int MODE, typename T, int BM, int BN, bool CONV1>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int FM = WM / 16, FN = WN / 16;
+template <int MODE, typename T, int BM, int BN, int WMW, int WNW, bool CONV1>
+__global__ void __launch_bounds__(64 * WMW * WNW) conv_gemm_kernel(const ConvArgs a) {
+  constexpr int NT = 64 * WMW * WNW;
+  constexpr int BK = Traits<T>::BK;
+  constexpr int KC = BK / 8;                 // 8-element chunks per k-tile row
+  constexpr int NSUB = BK / 32;              // 32-deep MFMA sub-steps per k step
+  constexpr int WTM = BM / WMW, WTN = BN / WNW;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr bool WG = (MODE == MODE_WGRAD);
-  constexpr int A_BYTES = WG ? 32 * MTile<T, BM>::ROW_BYTES : BM * KTile<T>::ROW_BYTES;
-  constexpr int B_BYTES = WG ? 32 * MTile<T, BN>::ROW_BYTES : BN * KTile<T>::ROW_BYTES;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int ITA = BM * 4 / 256;  // 8-element chunks per thread per k step
-  constexpr int ITB = BN * 4 / 256;
-  static_assert(ITA >= 1 && ITB >= 1, "tile too small");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  typedef Smem<MODE, T, BM, BN> SM;
+  constexpr int ITA = WG ? (BK * BM / 8) / NT : (BM * KC) / NT;
+  constexpr int ITB = WG ? (BK * BN / 8) / NT : (BN * KC) / NT;
+  static_assert(ITA >= 1 && ITB >= 1 && FM >= 1 && FN >= 1, "tile too small");
+  static_assert(!WG || ((BK * BM / 8) % NT == 0 && (BK * BN / 8) % NT == 0), "bad WGRAD tile");
+  __shared__ __attribute__((aligned(16))) char smem[SM::BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WNW, wn = wave % WNW;
 
   const int tn = blockIdx.x % a.tiles_n;
   const int tm = blockIdx.x / a.tiles_n;
@@ -224,25 +224,24 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
   const T* __restrict__ Bg = static_cast<const T*>(a.B);
 
   // ---------------- per-thread loader state ----------------
-  // FWD/DGRAD A: chunk (row, kc) with row = (tid + it*256) >> 2, kc = tid & 3
-  // B (FWD/DGRAD): same mapping over BN rows of the [Ng][Kg] weight matrix
-  // WGRAD A: [32 m][BM cols]: m_local = id / (BM/8), col chunk = id % (BM/8)
-  // WGRAD B: [32 m][BN cols]: m_local = id / (BN/8), col chunk = id % (BN/8)
+  // FWD/DGRAD: chunk id = tid + it*NT -> (row = id / KC, kc = id % KC); KC | NT so kc is fixed per thread
+  // WGRAD A: [BK m][BM cols]: ml = id / (BM/8), col chunk = id % (BM/8) (fixed per thread)
+  // WGRAD B: [BK m][BN cols]: ml = id / (BN/8), col chunk = id % (BN/8) (fixed per thread)
   int a_base[ITA], a_h[ITA], a_w[ITA];
   bool a_ok[ITA];
   int b_r = 0, b_s = 0, b_c = 0;
   bool b_colok = true;
-  const int kc = tid & 3;
+  const int kc = tid % KC;
 
   // uniform k-step counters (FWD/DGRAD):  k = ((r*S)+s)*Cred + cb
   int kr = 0, ks_ = 0, kcb = 0;
-  const int Cred = (MODE == MODE_FWD) ? a.C : a.K;  // contiguous reduction channels
+  const int Cred = (MODE == MODE_FWD) ? a.C : a.K;
 
   long mstart = 0, mend = 0;
   if constexpr (!WG) {
 #pragma unroll
     for (int it = 0; it < ITA; ++it) {
-      const int row = (tid + it * 256) >> 2;
+      const int row = (tid + it * NT) / KC;
       const int m = m0 + row;
       a_ok[it] = m < a.M;
       const int mm = a_ok[it] ? m : 0;
@@ -265,10 +264,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
       }
     }
   } else {
-    mstart = (long)blockIdx.y * a.ksteps * 32;
-    mend = mstart + (long)a.ksteps * 32;
+    mstart = (long)blockIdx.y * a.ksteps * BK;
+    mend = mstart + (long)a.ksteps * BK;
     if (mend > a.Mred) mend = a.Mred;
-    // B column info (fixed per thread): col chunk nc = tid % (BN/8)
     const int nc = tid % (BN / 8);
     const int col = n0 + nc * 8;
     b_colok = col < a.Ng;
@@ -293,10 +291,13 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int it = 0; it < ITA; ++it) {
         if constexpr (CONV1) {
-          // k step == filter row r; chunk kc = pixels s = 2kc, 2kc+1 (4 channels each)
-          const int hin = a_h[it] + ks;
-          const int w0 = a_w[it] + 2 * kc;
-          const bool rowok = a_ok[it] && hin >= 0 && hin < a.H;
+          // k = ks*BK + kc*8: filter row r = k / 32, pixel pair s = (k % 32) / 4, 4 channels each
+          const int k = ks * BK + kc * 8;
+          const int r = k >> 5;
+          const int s0 = (k & 31) >> 2;
+          const int hin = a_h[it] + r;
+          const int w0 = a_w[it] + s0;
+          const bool rowok = a_ok[it] && r < a.R && hin >= 0 && hin < a.H;
           const bool ok0 = rowok && w0 >= 0 && w0 < a.W;
           const bool ok1 = rowok && (w0 + 1) >= 0 && (w0 + 1) < a.W;
           const T* p0 = Ag + ((long)(a_base[it] + hin * a.W + w0)) * 4;
@@ -315,9 +316,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
         int p = hp, q = wp;
         bool ok = a_ok[it] && hp >= 0 && wp >= 0;
         if (a.stride != 1) {
-          ok = ok && (hp % a.stride == 0) && (wp % a.stride == 0);
-          p = hp / a.stride;
-          q = wp / a.stride;
+          ok = ok && ((hp | wp) & (a.stride - 1)) == 0;  // stride is a power of two (host-checked)
+          p = hp >> (a.stride >> 1);
+          q = wp >> (a.stride >> 1);
         }
         ok = ok && p < a.P && q < a.Q;
         const T* ptr = Ag + ((long)(a_base[it] + p * a.Q + q)) * a.K + kcb + kc * 8;
@@ -325,22 +326,21 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
       }
     }
     if constexpr (!WG) {
-      // B: [Ng][Kg] rows
 #pragma unroll
       for (int it = 0; it < ITB; ++it) {
-        const int row = (tid + it * 256) >> 2;
+        const int row = (tid + it * NT) / KC;
         const int n = n0 + row;
-        const bool ok = n < a.Ng;
-        const T* p = Bg + (long)(ok ? n : 0) * a.Kg + ks * 32 + kc * 8;
+        const int k = ks * BK + kc * 8;
+        const bool ok = n < a.Ng && k < a.Kg;
+        const T* p = Bg + (long)(ok ? n : 0) * a.Kg + (ok ? k : 0);
         load_v8<T>(rb[it], p, ok);
       }
     } else {
-      // A: dY[m][K] chunk along k;  B: X gathered chunk along (r,s,c)
 #pragma unroll
       for (int it = 0; it < ITA; ++it) {
-        const int id = tid + it * 256;
+        const int id = tid + it * NT;
         const int ml = id / (BM / 8), cch = id % (BM / 8);
-        const long m = mstart + (long)ks * 32 + ml;
+        const long m = mstart + (long)ks * BK + ml;
         const int k = m0 + cch * 8;
         const bool ok = m < mend && k < a.K;
         const T* p = Ag + (ok ? m : 0) * (long)a.K + (ok ? k : 0);
@@ -348,9 +348,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
       }
 #pragma unroll
       for (int it = 0; it < ITB; ++it) {
-        const int id = tid + it * 256;
+        const int id = tid + it * NT;
         const int ml = id / (BN / 8);
-        const long m = mstart + (long)ks * 32 + ml;
+        const long m = mstart + (long)ks * BK + ml;
         const bool mok = m < mend && b_colok;
         const int mm = mok ? (int)m : 0;
         const int n = fdiv(mm, a.div_pq);
@@ -377,7 +377,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
 
   auto advance_k = [&]() {  // uniform (r, s, cb) counters for FWD/DGRAD
     if constexpr (!WG && !CONV1) {
-      kcb += 32;
+      kcb += BK;
       if (kcb >= Cred) {
         kcb = 0;
         if (++ks_ >= a.S) { ks_ = 0; ++kr; }
@@ -386,22 +386,22 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
   };
 
   auto store_tiles = [&](int buf) {
-    char* As = smem + buf * STAGE;
-    char* Bs = As + A_BYTES;
+    char* As = smem + buf * SM::STAGE;
+    char* Bs = As + SM::A_BYTES;
     if constexpr (!WG) {
 #pragma unroll
-      for (int it = 0; it < ITA; ++it) store_kchunk<T>(As, (tid + it * 256) >> 2, kc, ra[it]);
+      for (int it = 0; it < ITA; ++it) store_kchunk(As, (tid + it * NT) / KC, kc, ra[it]);
 #pragma unroll
-      for (int it = 0; it < ITB; ++it) store_kchunk<T>(Bs, (tid + it * 256) >> 2, kc, rb[it]);
+      for (int it = 0; it < ITB; ++it) store_kchunk(Bs, (tid + it * NT) / KC, kc, rb[it]);
     } else {
 #pragma unroll
       for (int it = 0; it < ITA; ++it) {
-        const int id = tid + it * 256;
+        const int id = tid + it * NT;
         store_mchunk<BM>(As, id / (BM / 8), (id % (BM / 8)) * 8, ra[it]);
       }
 #pragma unroll
       for (int it = 0; it < ITB; ++it) {
-        const int id = tid + it * 256;
+        const int id = tid + it * NT;
         store_mchunk<BN>(Bs, id / (BN / 8), (id % (BN / 8)) * 8, rb[it]);
       }
     }
@@ -416,7 +416,7 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
   int nsteps = a.ksteps;
   if constexpr (WG) {
     const long rem = mend - mstart;
-    nsteps = rem > 0 ? (int)((rem + 31) / 32) : 0;
+    nsteps = rem > 0 ? (int)((rem + BK - 1) / BK) : 0;
   }
 
   if (nsteps > 0) {
@@ -431,31 +431,34 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
       load_tiles(ks + 1);
       advance_k();
     }
-    const char* As = smem + cur * STAGE;
-    const char* Bs = As + A_BYTES;
-    Frag<T> fa[FM], fb[FN];
-    if constexpr (!WG) {
+    const char* As = smem + cur * SM::STAGE;
+    const char* Bs = As + SM::A_BYTES;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) read_kfrag(fa[i], As, wm * WM + i * 16 + (lane & 15), lane >> 4);
+    for (int h = 0; h < NSUB; ++h) {
+      Frag<T> fa[FM], fb[FN];
+      if constexpr (!WG) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) read_kfrag(fb[j], Bs, wn * WN + j * 16 + (lane & 15), lane >> 4);
-    } else {
+        for (int i = 0; i < FM; ++i) read_kfrag(fa[i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[i], As, wm * WM + i * 16, lane);
+        for (int j = 0; j < FN; ++j) read_kfrag(fb[j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, h);
+      } else {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[j], Bs, wn * WN + j * 16, lane);
+        for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[i], As, wm * WTM + i * 16, lane, h);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[j], Bs, wn * WTN + j * 16, lane, h);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
     }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
     if (ks + 1 < nsteps) store_tiles(cur ^ 1);
     __syncthreads();
   }
 
   // ---------------- epilogue ----------------
-  const int rbase = wm * WM + (lane >> 4) * 4;
-  const int cbase = wn * WN + (lane & 15);
+  const int rbase = wm * WTM + (lane >> 4) * 4;
+  const int cbase = wn * WTN + (lane & 15);
   if constexpr (MODE == MODE_WGRAD) {
     float* slab = static_cast<float*>(a.out) + (long)blockIdx.y * a.M * a.Ng;
 #pragma unroll
@@ -473,32 +476,57 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
     return;
   }
 
-  // Out and Add may alias (in-place residual-gradient add): no __restrict__
-  T* Out = static_cast<T*>(a.out);
-  const T* Add = static_cast<const T*>(a.add);
+  // stage the tile through LDS (main loop finished: the staging buffers are free)
+  constexpr int EROW = BN * (int)sizeof(T) + 16;  // padded row (bytes)
+  {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + cbase + j * 16;
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + rbase + i * 16 + e;
-        if (m < a.M && n < a.Ng) {
-          float v = acc[i][j][e];
-          if constexpr (MODE == MODE_DGRAD) {
-            if (Add) v += to_f32<T>(Add[(long)m * a.Ng + n]);
-          }
-          Out[(long)m * a.Ng + n] = from_f32<T>(v);
+        for (int e = 0; e < 4; ++e) {
+          const int row = rbase + i * 16 + e;
+          const int col = cbase + j * 16;
+          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) = from_f32<T>(acc[i][j][e]);
+        }
+  }
+  __syncthreads();
+  {
+    // each thread moves 8-element chunks: BN/8 chunks per row
+    constexpr int CPR = BN / 8;
+    T* Out = static_cast<T*>(a.out);   // may alias Add (in-place residual-gradient add)
+    const T* Add = static_cast<const T*>(a.add);
+    for (int id = tid; id < BM * CPR; id += NT) {
+      const int row = id / CPR, ch = id % CPR;
+      const int m = m0 + row, n = n0 + ch * 8;
+      if (m >= a.M || n >= a.Ng) continue;
+      Vec8<T> v;
+      const char* src = smem + row * EROW + ch * 8 * (int)sizeof(T);
+      if constexpr (sizeof(T) == 2) {
+        v.v = *reinterpret_cast<const i32x4*>(src);
+      } else {
+        reinterpret_cast<Vec8<float>&>(v).v0 = reinterpret_cast<const i32x4*>(src)[0];
+        reinterpret_cast<Vec8<float>&>(v).v1 = reinterpret_cast<const i32x4*>(src)[1];
+      }
+      if constexpr (MODE == MODE_DGRAD) {
+        if (Add) {
+          // the unrounded accumulator would be better; the LDS copy is already in T
+          Vec8<T> r;
+          r.load(Add + (long)m * a.Ng + n);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v.set(j, v.get(j) + r.get(j));
         }
       }
+      v.store(Out + (long)m * a.Ng + n);
     }
+  }
 
   if constexpr (MODE == MODE_FWD) {
     if (a.partial == nullptr) return;
-    // BatchNorm partial statistics over this tile's valid rows.
-    float* red = reinterpret_cast<float*>(smem);  // [2][BN]  (main loop finished: safe to reuse)
-    float* mean_t = red + 2 * BN;                  // [BN]
+    __syncthreads();
+    // BatchNorm partial statistics over this tile's valid rows (from fp32 accumulators).
+    float* red = reinterpret_cast<float*>(smem);  // [WMW][BN]
+    float* mean_t = red + WMW * BN;               // [BN]
     const int cnt = min(BM, a.M - m0);
     float s[FN];
 #pragma unroll
@@ -520,7 +548,12 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
       for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = s[j];
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) mean_t[c] = (red[c] + red[BN + c]) / (float)cnt;
+    for (int c = tid; c < BN; c += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+      mean_t[c] = t / (float)cnt;
+    }
     __syncthreads();
     float q2[FN];
 #pragma unroll
@@ -544,16 +577,18 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = q2[j];
     }
-    // sums were overwritten: recompute from mean
     __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
+    const int tiles_m = gridDim.x / a.tiles_n;
+    for (int c = tid; c < BN; c += NT) {
       const int n = n0 + c;
       if (n < a.Ng) {
-        const int tiles_m = gridDim.x / a.tiles_n;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
         float* rec = a.partial + ((long)n * tiles_m + tm) * 3;  // [C][tiles][3]
         rec[0] = (float)cnt;
         rec[1] = mean_t[c] * (float)cnt;
-        rec[2] = red[c] + red[BN + c];
+        rec[2] = t;
       }
     }
   }
@@ -561,25 +596,39 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a) {
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
 //   (accumulate ? dW : 0) + sum_split slab[split][k][(r*Sp + s)*Cp + c]
-// Threads walk the slab in its own (k, col) order so every split's read is
-// coalesced; padded columns (s >= S or c >= C) are skipped.
+// Block = 32 output elements x 8 split groups; each group sums a contiguous
+// split range in order, the 8 partials are combined in fixed order in LDS.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int Ng, int C, int R,
                                     int S, int Cp, int Sp, float* __restrict__ dw, int accumulate) {
+  __shared__ float red[8][33];
   const long total = (long)K * Ng;
   const long sstride = (long)K * Ng;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+  const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const long idx = (long)blockIdx.x * 32 + el;
+  const int per = (splits + 7) / 8;
+  const int s0 = grp * per;
+  const int s1 = min(splits, s0 + per);
+  float acc = 0.f;
+  if (idx < total) {
+    const float* p = slab + idx;
+    for (int sp = s0; sp < s1; ++sp) acc += p[sp * sstride];
+  }
+  red[grp][el] = acc;
+  __syncthreads();
+  if (grp == 0 && idx < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][el];
     const int col = (int)(idx % Ng);
     const int k = (int)(idx / Ng);
     const int c = col % Cp;
     const int rs = col / Cp;
     const int s = rs % Sp;
     const int r = rs / Sp;
-    if (c >= C || s >= S) continue;
-    float acc = 0.f;
-    const float* p = slab + idx;
-    for (int sp = 0; sp < splits; ++sp) acc += p[sp * sstride];
-    const long o = (((long)k * C + c) * R + r) * S + s;
-    dw[o] = accumulate ? dw[o] + acc : acc;
+    if (c < C && s < S) {
+      const long o = (((long)k * C + c) * R + r) * S + s;
+      dw[o] = accumulate ? dw[o] + t : t;
+    }
   }
 }
 
@@ -588,7 +637,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
 // ---------------------------------------------------------------------------
 struct Plan {
   int mode;
-  int bm, bn;
+  int bm, bn, wmw, wnw;
   bool conv1;
   ConvArgs args;
   dim3 grid;
@@ -610,18 +659,30 @@ static void fill_common(ConvArgs& a, const ssip_conv_desc* d) {
   a.div_w = make_fastdiv((uint32_t)d->W);
 }
 
-static int plan_conv(int mode, const ssip_conv_desc* d, Plan& pl) {
+static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
+  // bf16: 256-row tiles (8 waves) when the grid still fills the chip twice over
+  const int bn = (Ng % 128 == 0) ? 128 : 64;
+  const long blocks256 = (long)ceil_div(M, 256) * ceil_div(Ng, bn);
+  if (elem_bytes == 2 && blocks256 >= 512) {
+    pl.bm = 256; pl.bn = bn; pl.wmw = 4; pl.wnw = 2;
+  } else {
+    pl.bm = 128; pl.bn = bn; pl.wmw = 2; pl.wnw = 2;
+  }
+}
+
+static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl) {
   SSIP_REQUIRE(desc_ok(d), SSIP_ERR_ARG, "bad conv descriptor");
-  // output size must match the conv formula
   pl.mode = mode;
   pl.conv1 = (d->C == 4);
   // the padded stem stores S = 8 columns for a real 7-wide filter
   const int s_real = pl.conv1 ? d->S - 1 : d->S;
   SSIP_REQUIRE(d->P == (d->H + 2 * d->pad - d->R) / d->stride + 1 && d->Q == (d->W + 2 * d->pad - s_real) / d->stride + 1,
                SSIP_ERR_ARG, "P/Q inconsistent with H/W/R/S/stride/pad");
-  SSIP_REQUIRE(pl.conv1 ? (d->S == 8) : (d->C % 32 == 0), SSIP_ERR_ARG,
-               "conv input channels must be a multiple of 32 (or 4 with S padded to 8); got C=%d S=%d", d->C, d->S);
-  SSIP_REQUIRE(d->K % 32 == 0, SSIP_ERR_ARG, "conv output channels must be a multiple of 32; got K=%d", d->K);
+  const int BK = elem_bytes == 2 ? 64 : 32;
+  SSIP_REQUIRE(pl.conv1 ? (d->S == 8) : (d->C % BK == 0), SSIP_ERR_ARG,
+               "conv input channels must be a multiple of %d (or 4 with S padded to 8); got C=%d S=%d", BK, d->C,
+               d->S);
+  SSIP_REQUIRE(d->K % BK == 0, SSIP_ERR_ARG, "conv output channels must be a multiple of %d; got K=%d", BK, d->K);
   const long NPQ = (long)d->N * d->P * d->Q, NHW = (long)d->N * d->H * d->W;
   SSIP_REQUIRE(NPQ < (1l << 31) && NHW * d->C < (1l << 31) && NPQ * d->K < (1l << 31), SSIP_ERR_ARG,
                "tensor too large for 32-bit indexing");
@@ -630,28 +691,30 @@ static int plan_conv(int mode, const ssip_conv_desc* d, Plan& pl) {
   pl.splits = 1;
   if (mode == MODE_FWD) {
     a.M = (int)NPQ; a.Ng = d->K; a.Kg = d->R * d->S * d->C;
-    a.ksteps = a.Kg / 32;
-    pl.bm = 128; pl.bn = (d->K % 128 == 0) ? 128 : 64;
+    a.ksteps = ceil_div(a.Kg, BK);
+    pick_tile(a.M, a.Ng, elem_bytes, pl);
   } else if (mode == MODE_DGRAD) {
     SSIP_REQUIRE(!pl.conv1, SSIP_ERR_ARG, "dgrad of the C=4 stem conv is not supported (input needs no grad)");
+    SSIP_REQUIRE(d->stride == 1 || d->stride == 2 || d->stride == 4, SSIP_ERR_ARG, "dgrad stride must be 1, 2 or 4");
     a.M = (int)NHW; a.Ng = d->C; a.Kg = d->R * d->S * d->K;
-    a.ksteps = a.Kg / 32;
-    pl.bm = 128; pl.bn = (d->C % 128 == 0) ? 128 : 64;
+    a.ksteps = a.Kg / BK;
+    pick_tile(a.M, a.Ng, elem_bytes, pl);
   } else {
     a.M = d->K; a.Ng = d->R * d->S * d->C; a.Kg = 0;
     a.Mred = (int)NPQ;
+    pl.wmw = 2; pl.wnw = 2;
     pl.bm = (d->K % 128 == 0) ? 128 : 64;
     pl.bn = 128;
     if (a.Ng % 128 != 0 && a.Ng % 64 == 0 && pl.bm == 128) pl.bn = 64;
     const int tiles = ceil_div(a.M, pl.bm) * ceil_div(a.Ng, pl.bn);
-    const int total_ks = ceil_div(a.Mred, 32);
+    const int total_ks = ceil_div(a.Mred, BK);
     // ~1024 blocks (4 per CU), slab <= 64 MiB (stays in the Infinity Cache),
-    // >= 8 k-steps per split
+    // >= 16 k-steps per split (keeps the slab and its reduction small)
     int splits = ceil_div(1024, tiles);
     const long slab_split = (long)a.M * a.Ng * 4;
     const int cap_bytes = (int)std::max<long>(1, (64l << 20) / slab_split);
     if (splits > cap_bytes) splits = cap_bytes;
-    const int max_splits = ceil_div(total_ks, 8);
+    const int max_splits = std::max(1, total_ks / 16);
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
     a.ksteps = ceil_div(total_ks, splits);
@@ -666,49 +729,87 @@ static int plan_conv(int mode, const ssip_conv_desc* d, Plan& pl) {
 
 template <int MODE, typename T>
 static int launch_conv(const Plan& pl, hipStream_t st) {
-#define SSIP_LAUNCH(BM_, BN_, C1_) \
-  { hipLaunchKernelGGL((conv_gemm_kernel<MODE, T, BM_, BN_, C1_>), pl.grid, dim3(256), 0, st, pl.args); }
+#define SSIP_LAUNCH(BM_, BN_, WM_, WN_, C1_)                                                                  \
+  {                                                                                                           \
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, T, BM_, BN_, WM_, WN_, C1_>), pl.grid, dim3(64 * WM_ * WN_), 0, \
+                       st, pl.args);                                                                          \
+  }
   const bool c1 = pl.conv1;
-  if (pl.bm == 128 && pl.bn == 128) {
-    if constexpr (MODE != MODE_DGRAD) { if (c1) SSIP_LAUNCH(128, 128, true) else SSIP_LAUNCH(128, 128, false) }
-    else SSIP_LAUNCH(128, 128, false)
-  } else if (pl.bm == 128 && pl.bn == 64) {
-    if constexpr (MODE != MODE_DGRAD) { if (c1) SSIP_LAUNCH(128, 64, true) else SSIP_LAUNCH(128, 64, false) }
-    else SSIP_LAUNCH(128, 64, false)
-  } else if (pl.bm == 64 && pl.bn == 128 && MODE == MODE_WGRAD) {
-    if (c1) SSIP_LAUNCH(64, 128, true) else SSIP_LAUNCH(64, 128, false)
+  if constexpr (MODE == MODE_WGRAD) {
+    if (pl.bm == 128 && pl.bn == 128) {
+      if (c1) SSIP_LAUNCH(128, 128, 2, 2, true) else SSIP_LAUNCH(128, 128, 2, 2, false)
+    } else if (pl.bm == 128 && pl.bn == 64) {
+      if (c1) SSIP_LAUNCH(128, 64, 2, 2, true) else SSIP_LAUNCH(128, 64, 2, 2, false)
+    } else if (pl.bm == 64 && pl.bn == 128) {
+      if (c1) SSIP_LAUNCH(64, 128, 2, 2, true) else SSIP_LAUNCH(64, 128, 2, 2, false)
+    } else {
+      ::ssip::set_error("no wgrad kernel for tile %dx%d", pl.bm, pl.bn);
+      return SSIP_ERR_ARG;
+    }
+  } else if constexpr (MODE == MODE_FWD) {
+    if (sizeof(T) == 2 && pl.bm == 256 && pl.bn == 128) {
+      if constexpr (sizeof(T) == 2) { if (c1) SSIP_LAUNCH(256, 128, 4, 2, true) else SSIP_LAUNCH(256, 128, 4, 2, false) }
+    } else if (sizeof(T) == 2 && pl.bm == 256 && pl.bn == 64) {
+      if constexpr (sizeof(T) == 2) { if (c1) SSIP_LAUNCH(256, 64, 4, 2, true) else SSIP_LAUNCH(256, 64, 4, 2, false) }
+    } else if (pl.bm == 128 && pl.bn == 128) {
+      if (c1) SSIP_LAUNCH(128, 128, 2, 2, true) else SSIP_LAUNCH(128, 128, 2, 2, false)
+    } else if (pl.bm == 128 && pl.bn == 64) {
+      if (c1) SSIP_LAUNCH(128, 64, 2, 2, true) else SSIP_LAUNCH(128, 64, 2, 2, false)
+    } else {
+      ::ssip::set_error("no fwd kernel for tile %dx%d", pl.bm, pl.bn);
+      return SSIP_ERR_ARG;
+    }
   } else {
-    ::ssip::set_error("no kernel for tile %dx%d", pl.bm, pl.bn);
-    return SSIP_ERR_ARG;
+    if (sizeof(T) == 2 && pl.bm == 256 && pl.bn == 128) {
+      if constexpr (sizeof(T) == 2) SSIP_LAUNCH(256, 128, 4, 2, false)
+    } else if (sizeof(T) == 2 && pl.bm == 256 && pl.bn == 64) {
+      if constexpr (sizeof(T) == 2) SSIP_LAUNCH(256, 64, 4, 2, false)
+    } else if (pl.bm == 128 && pl.bn == 128) SSIP_LAUNCH(128, 128, 2, 2, false)
+    else if (pl.bm == 128 && pl.bn == 64) SSIP_LAUNCH(128, 64, 2, 2, false)
+    else {
+      ::ssip::set_error("no dgrad kernel for tile %dx%d", pl.bm, pl.bn);
+      return SSIP_ERR_ARG;
+    }
   }
 #undef SSIP_LAUNCH
   return ::ssip::check_launch("conv_gemm");
 }
+
+static int elem_bytes_of(int dtype) { return dtype == SSIP_BF16 ? 2 : 4; }
 
 }  // namespace
 
 extern "C" {
 
 int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d) {
+  // the partial-buffer size must not depend on dtype: size for the smaller (128-row) tiles
   Plan pl;
-  if (plan_conv(MODE_FWD, d, pl) != SSIP_OK) return -1;
-  return (int64_t)ceil_div(pl.args.M, pl.bm) * d->K * 3;
+  if (plan_conv(MODE_FWD, d, 4, pl) != SSIP_OK) {
+    if (plan_conv(MODE_FWD, d, 2, pl) != SSIP_OK) return -1;
+  }
+  return (int64_t)ceil_div(pl.args.M, 128) * d->K * 3;
 }
 
 int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, void* y, float* bn_partial,
                   void* stream) {
   Plan pl;
-  int rc = plan_conv(MODE_FWD, d, pl);
+  int rc = plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
   SSIP_REQUIRE(x && w_krsc && y, SSIP_ERR_ARG, "ssip_conv_fwd: null pointer");
   pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_FWD, T>(pl, (hipStream_t)stream));
 }
 
+int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
+  Plan pl;
+  if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
+  return ceil_div(pl.args.M, pl.bm);
+}
+
 int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, void* dx,
                     const void* dx_add, void* stream) {
   Plan pl;
-  int rc = plan_conv(MODE_DGRAD, d, pl);
+  int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
   SSIP_REQUIRE(dy && w_crsk && dx, SSIP_ERR_ARG, "ssip_conv_dgrad: null pointer");
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
@@ -716,15 +817,19 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
 }
 
 int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d) {
-  Plan pl;
-  if (plan_conv(MODE_WGRAD, d, pl) != SSIP_OK) return -1;
-  return (int64_t)pl.splits * pl.args.M * pl.args.Ng * 4;
+  // max over dtypes so one workspace serves both
+  Plan p2, p4;
+  int64_t b = -1;
+  if (plan_conv(MODE_WGRAD, d, 2, p2) == SSIP_OK) b = (int64_t)p2.splits * p2.args.M * p2.args.Ng * 4;
+  if (plan_conv(MODE_WGRAD, d, 4, p4) == SSIP_OK)
+    b = std::max<int64_t>(b, (int64_t)p4.splits * p4.args.M * p4.args.Ng * 4);
+  return b;
 }
 
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
                     int s_real, int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
   Plan pl;
-  int rc = plan_conv(MODE_WGRAD, d, pl);
+  int rc = plan_conv(MODE_WGRAD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
   SSIP_REQUIRE(dy && x && dw_kcrs && workspace, SSIP_ERR_ARG, "ssip_conv_wgrad: null pointer");
   const int64_t need = (int64_t)pl.splits * pl.args.M * pl.args.Ng * 4;
@@ -736,9 +841,9 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   SSIP_DISPATCH_DTYPE(dtype, T, rc = launch_conv<MODE_WGRAD, T>(pl, st));
   if (rc) return rc;
   const long total = (long)d->K * pl.args.Ng;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)workspace, pl.splits, d->K,
-                     pl.args.Ng, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, st,
+                     (const float*)workspace, pl.splits, d->K, pl.args.Ng, c_real, d->R, s_real, d->C, d->S, dw_kcrs,
+                     accumulate);
   return ::ssip::check_launch("wgrad_reduce");
 }
 

@@ -55,6 +55,7 @@ _SIGS = {
     "ssip_last_error": (ctypes.c_char_p, []),
     "ssip_version": (_c_int, []),
     "ssip_conv_fwd_partial_floats": (_c_i64, [_PD]),
+    "ssip_conv_fwd_partial_tiles": (_c_int, [_PD, _c_int]),
     "ssip_conv_fwd": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_wgrad_workspace_bytes": (_c_i64, [_PD]),
@@ -114,6 +115,6 @@ def check(rc: int, what: str) -> None:
 def call(name: str, *args) -> int:
     fn = getattr(lib(), name)
     rc = fn(*args)
-    if _SIGS[name][0] is _c_int and name not in ("ssip_version",):
+    if _SIGS[name][0] is _c_int and name not in ("ssip_version", "ssip_conv_fwd_partial_tiles"):
         check(rc, name)
     return rc

@@ -135,6 +135,44 @@ def encode_params(draws: Sequence[AugDraw], w: int, h: int) -> torch.Tensor:
     return torch.tensor([d.encode(w, h) for d in draws], dtype=torch.int32)
 
 
+def draw_params_batch(n: int, size: int, strong: bool, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """Vectorised parameter draw for synthetic batches (bench): same
+    distributions as draw_train_params / draw_strong_params, fixed-point
+    terms computed with numpy in float64 (the 15-digit rounding Pillow
+    applies is skipped — irrelevant for synthetic inputs)."""
+    deg = 30.0 if strong else 10.0
+    flip = (torch.rand(n, generator=generator) < 0.5).numpy()
+    ang = (torch.rand(n, generator=generator, dtype=torch.float64) * 2 * deg - deg).numpy()
+    a = -np.radians(ang % 360.0)
+    c, s_ = np.cos(a), np.sin(a)
+    cx = cy = size / 2
+    m2 = c * (-cx) + s_ * (-cy) + cx
+    m5 = -s_ * (-cx) + c * (-cy) + cy
+
+    def fix(v):
+        return np.floor(v * 65536.0 + 0.5).astype(np.int64)
+
+    p = np.zeros((n, PARAM_FIELDS), np.int64)
+    p[:, 0] = flip
+    p[:, 1] = 1
+    p[:, 2], p[:, 3], p[:, 4], p[:, 5] = fix(c), fix(s_), fix(-s_), fix(c)
+    p[:, 6] = fix(m2 + s_ * 0.5 + c * 0.5)
+    p[:, 7] = fix(m5 + c * 0.5 - s_ * 0.5)
+    one = np.array(1.0, np.float32).view(np.int32)
+    p[:, 9] = one
+    p[:, 10] = one
+    if strong:
+        u = torch.rand(n, 4, generator=generator).numpy()
+        p[:, 8] = 1
+        p[:, 9] = (1.0 + 0.4 * (2 * u[:, 0] - 1)).astype(np.float32).view(np.int32)
+        p[:, 10] = (1.0 + 0.4 * (2 * u[:, 1] - 1)).astype(np.float32).view(np.int32)
+        side = max(1, int(0.25 * size))
+        x0 = (u[:, 2] * (size - side)).astype(np.int64)
+        y0 = (u[:, 3] * (size - side)).astype(np.int64)
+        p[:, 11], p[:, 12], p[:, 13], p[:, 14] = x0, y0, x0 + side, y0 + side
+    return torch.from_numpy(p.astype(np.int32))
+
+
 # ---------------------------------------------------------------------------
 # the transform
 # ---------------------------------------------------------------------------
@@ -178,7 +216,8 @@ class GpuTransform:
         c = self.crop
         return Hr, Wr, c, c, int(round((Wr - c) / 2.0)), int(round((Hr - c) / 2.0))
 
-    def __call__(self, images: torch.Tensor, params: Optional[torch.Tensor] = None) -> DeviceImages:
+    def __call__(self, images: torch.Tensor, params: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None) -> DeviceImages:
         if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] != 3:
             raise ValueError("GpuTransform expects uint8 [B,H,W,3]")
         if not images.is_cuda:
@@ -199,7 +238,10 @@ class GpuTransform:
         kv, bv, cv = 0, None, None
         if Hr != H:
             bv, cv, kv = self._table(H, Hr, dev)
-        out = torch.empty((B, Ho, Wo, 4), device=dev, dtype=self.dtype)
+        if out is None:
+            out = torch.empty((B, Ho, Wo, 4), device=dev, dtype=self.dtype)
+        elif out.shape != (B, Ho, Wo, 4) or out.dtype != self.dtype or not out.is_contiguous():
+            raise ValueError("GpuTransform: bad `out` buffer")
         pptr = None
         if params is not None:
             params = params.to(dev, torch.int32).contiguous()

@@ -1,0 +1,120 @@
+"""Data parallelism over RCCL (torch.distributed backend "nccl" on ROCm).
+
+The reference is single-device (no collectives); this is the
+build's DP extension for configs 4/5.  One process per GPU; each rank runs
+the full train step on its own shard of the batch; the only exchange is an
+all-reduce of the flat fp32 gradient arena (44.7 MB for ResNet-18).
+
+Bucketing: the arena is cut at parameter boundaries into buckets of about
+`bucket_bytes`.  The engine's backward calls `mark_ready(params)` as each
+block's gradients are enqueued (layer4 first); a bucket whose parameters are
+all ready is all-reduced immediately with `async_op=True`, so RCCL runs on
+its own stream over xGMI while the remaining backward kernels run.  The
+1/world average is folded into the AdamW launch (grad_scale), so no extra
+pass over the gradients is needed.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend: Optional[str] = None):
+    """Initialise the default process group from torchrun's env (127.0.0.1
+    rendezvous).  Returns (rank, world, local_rank)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local
+
+
+class GradBucketer:
+    def __init__(self, arena, bucket_bytes: int = 16 << 20, group=None):
+        self.arena = arena
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # buckets in reverse parameter order (the backward produces the last params first)
+        params = list(arena.params)
+        spans = [arena.span(p) for p in params]
+        buckets: List[List[int]] = []
+        cur: List[int] = []
+        cur_bytes = 0
+        for i in range(len(params) - 1, -1, -1):
+            cur.append(i)
+            cur_bytes += spans[i][1] * 4
+            if cur_bytes >= bucket_bytes:
+                buckets.append(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            buckets.append(cur)
+        self.params = params
+        self.buckets = buckets
+        self.bucket_of = {}
+        for b, idxs in enumerate(buckets):
+            for i in idxs:
+                self.bucket_of[id(params[i])] = b
+        self.ranges = []
+        for idxs in buckets:
+            lo = min(spans[i][0] for i in idxs)
+            hi = max(spans[i][0] + spans[i][1] for i in idxs)
+            self.ranges.append((lo, hi))
+        self.reset()
+
+    def reset(self):
+        self.pending = [set(i for i in idxs if self.params[i].requires_grad) for idxs in self.buckets]
+        self.handles = []
+        self.launched = [False] * len(self.buckets)
+
+    def _launch(self, b: int):
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        lo, hi = self.ranges[b]
+        if self.world > 1:
+            self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                                async_op=True))
+
+    def mark_ready(self, params) -> None:
+        idx = {id(p): i for i, p in enumerate(self.params)}
+        for p in params:
+            b = self.bucket_of.get(id(p))
+            if b is None:
+                continue
+            self.pending[b].discard(idx[id(p)])
+            if not self.pending[b]:
+                self._launch(b)
+
+    def finish(self) -> float:
+        """Launch anything left, wait, and return the grad scale (1/world)."""
+        for b in range(len(self.buckets)):
+            if any(self.params[i].requires_grad for i in self.buckets[b]):
+                self._launch(b)
+        for h in self.handles:
+            h.wait()
+        self.handles = []
+        return 1.0 / self.world
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous shard [lo, hi) of n items for `rank` (pseudo-labelling,
+    evaluation and embedding extraction shard the file list this way)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def strided_indices(indices: List[int], rank: int, world: int) -> List[int]:
+    """Rank-stride a global sample stream (the WeightedRandomSampler draw is
+    generated identically on every rank from the same seed)."""
+    return list(indices[rank::world])

@@ -39,6 +39,42 @@ def stream_ptr() -> int:
 
 
 # ---------------------------------------------------------------------------
+# optional per-launch timing of the conv kernels (bench.py's roofline leg):
+# HIP events recorded on the stream the kernels are launched on.
+# ---------------------------------------------------------------------------
+class ConvTimer:
+    def __init__(self):
+        self.records = []  # (kind, flops, start_event, end_event)
+
+    def wrap(self, kind: str, flops: int, fn, *args):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn(*args)
+        e.record()
+        self.records.append((kind, flops, s, e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, flops, s, e in self.records:
+            ms = s.elapsed_time(e)
+            d = out.setdefault(kind, [0, 0.0, 0])
+            d[0] += flops
+            d[1] += ms
+            d[2] += 1
+        return out
+
+
+_timer = None
+
+
+def set_conv_timer(t):
+    global _timer
+    _timer = t
+
+
+# ---------------------------------------------------------------------------
 # convolution
 # ---------------------------------------------------------------------------
 @dataclass(frozen=True)
@@ -77,6 +113,13 @@ def conv_fwd_partial_floats(g: ConvGeom) -> int:
     return int(_lib.lib().ssip_conv_fwd_partial_floats(g.desc()))
 
 
+def conv_fwd_partial_tiles(g: ConvGeom, dtype: torch.dtype) -> int:
+    t = int(_lib.lib().ssip_conv_fwd_partial_tiles(g.desc(), _DT[dtype]))
+    if t <= 0:
+        raise RuntimeError(_lib.lib().ssip_last_error().decode())
+    return t
+
+
 def conv_fwd(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor,
              partial: Optional[torch.Tensor] = None) -> None:
     assert x.numel() == g.N * g.H * g.W * g.C, "conv_fwd: x shape"
@@ -86,6 +129,10 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor
     if partial is not None:
         assert partial.dtype == torch.float32 and partial.numel() >= conv_fwd_partial_floats(g)
     d = g.desc()
+    if _timer is not None:
+        _timer.wrap("fwd", g.flops(), call, "ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial),
+                    stream_ptr())
+        return
     call("ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial), stream_ptr())
 
 
@@ -96,7 +143,11 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx: torch.Te
     assert dx.numel() == g.N * g.H * g.W * g.C, "conv_dgrad: dx shape"
     if dx_add is not None:
         assert dx_add.numel() == dx.numel() and dx_add.dtype == dx.dtype
-    call("ssip_conv_dgrad", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx), _p(dx_add), stream_ptr())
+    args = ("ssip_conv_dgrad", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx), _p(dx_add), stream_ptr())
+    if _timer is not None:
+        _timer.wrap("dgrad", g.flops(), call, *args)
+        return
+    call(*args)
 
 
 def conv_wgrad_workspace_bytes(g: ConvGeom) -> int:
@@ -108,8 +159,12 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
     assert dy.numel() == g.N * g.P * g.Q * g.K and x.numel() == g.N * g.H * g.W * g.C
     assert dw.dtype == torch.float32 and dw.numel() == g.K * g.c_real * g.R * g.s_real
     nbytes = workspace.numel() * workspace.element_size()
-    call("ssip_conv_wgrad", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real, int(accumulate),
-         _p(workspace), nbytes, stream_ptr())
+    args = ("ssip_conv_wgrad", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real,
+            int(accumulate), _p(workspace), nbytes, stream_ptr())
+    if _timer is not None:
+        _timer.wrap("wgrad", g.flops(), call, *args)
+        return
+    call(*args)
 
 
 def weight_prep(w: torch.Tensor, dtype: torch.dtype, Cp: int, Sp: int, krsc: Optional[torch.Tensor],

@@ -53,7 +53,7 @@ class AdamW(torch.optim.Optimizer):
         return runs, loose
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, grad_scale: float = 1.0):
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -82,9 +82,9 @@ class AdamW(torch.optim.Optimizer):
                 step = int(self.state[ps[0]]["step"].item())
                 ops.adamw(self.arena.flat[off:off + n], self.arena.grad[off:off + n],
                           self._flat_state[0][off:off + n], self._flat_state[1][off:off + n],
-                          group["lr"], b1, b2, group["eps"], group["weight_decay"], step)
+                          group["lr"], b1, b2, group["eps"], group["weight_decay"], step, grad_scale)
             for p in loose:
                 st = self.state[p]
                 ops.adamw(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
-                          group["eps"], group["weight_decay"], int(st["step"].item()))
+                          group["eps"], group["weight_decay"], int(st["step"].item()), grad_scale)
         return loss

@@ -234,6 +234,10 @@ class SSIPResNet(nn.Module):
                 raise ValueError(f"expected a [B,3,H,W] batch, got {tuple(x.shape)}")
             images = ops.nchw_to_nhwc(x, 4, self.compute_dtype)
         params = [p for p in self.parameters()]
+        if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
+            # inference (eval, pseudo-labelling, weak view, extraction): no autograd node, nothing saved
+            sv = _forward(self, images, train=self.training, save=False)
+            return sv.feat.view(sv.N, -1, 1, 1) if self.embedding_only else sv.logits
         return _NetFn.apply(self, images, *params)
 
 
@@ -241,11 +245,7 @@ class _NetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model: SSIPResNet, images: torch.Tensor, *params):
         train = model.training
-        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-        # note: inside autograd.Function.forward grad mode is disabled; the
-        # decision is taken from the inputs' requires_grad
-        need_grad = any(p.requires_grad for p in params)
-        saved = _forward(model, images, train=train, save=need_grad and train)
+        saved = _forward(model, images, train=train, save=train)
         ctx.model = model
         ctx.saved = saved
         out = saved.feat.view(saved.N, -1, 1, 1) if model.embedding_only else saved.logits
@@ -301,7 +301,7 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
         nparts = ops.conv_fwd_partial_floats(g)
         partial = torch.empty(nparts, device=x.device, dtype=torch.float32)
         ops.conv_fwd(g, x, krsc, y, partial)
-        ops.bn_finalize(g.K, nparts // (3 * g.K), partial, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+        ops.bn_finalize(g.K, ops.conv_fwd_partial_tiles(g, dt), partial, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                         bn.running_var, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
                         update_running, stats[0], stats[1], stats[2], stats[3])
     else:
@@ -419,15 +419,20 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         dw, accw = _grad_target(fc_w, arena)
     if fc.bias is not None and fc.bias.requires_grad:
         db, accb = _grad_target(fc.bias, arena)
+    hook = getattr(model, "grad_ready_hook", None)
     if not trunk_trainable:
         if dw is not None:
             ops.avgpool_fc_bwd(dt, N, sv.last_pq, C, J, dlogits, fc_w.detach(), sv.feat, None, dw,
                                db, accw)
+        if hook is not None:
+            hook(list(fc.parameters()))
         return
     dz = torch.empty_like(sv.last)
     if dw is not None and db is not None and accw != accb:
         raise RuntimeError("ssip: fc weight/bias grads must both be fresh or both accumulate")
     ops.avgpool_fc_bwd(dt, N, sv.last_pq, C, J, dlogits, fc_w.detach(), sv.feat, dz, dw, db, accw)
+    if hook is not None:
+        hook(list(fc.parameters()))
 
     # earliest trainable stage decides where dgrad can stop
     stage_params = [[model.conv1, model.bn1]] + [[m for m in b.modules() if m is not b] for b in model.blocks()]
@@ -476,6 +481,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         ops.conv_dgrad(rec.geom, dy, crsk, out, add)
 
     nblocks = len(sv.blocks)
+    blocks = list(model.blocks())
     for bi in range(nblocks - 1, -1, -1):
         recs, ds, xin = sv.blocks[bi]
         stage_idx = bi + 1
@@ -508,6 +514,8 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
             conv_wgrad(ds, dy_ds)
             if dxin is not None:
                 conv_dgrad(ds, dy_ds, dxin, dxin)
+        if hook is not None:
+            hook(list(blocks[bi].parameters()))
         dz = dxin
         if dz is None:
             return
@@ -519,6 +527,8 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     ops.maxpool_bwd(N, P1, Q1, stem.geom.K, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, dz1)
     dy1 = bn_backward(stem, dz1, stem.z)
     conv_wgrad(stem, dy1)
+    if hook is not None:
+        hook([model.conv1.weight, model.bn1.weight, model.bn1.bias])
 
 
 def _prepped_t(model: SSIPResNet, rec: _ConvRec):

@@ -16,7 +16,7 @@ SHAPES = [
     (2, 64, 16, 16, 64, 3, 1, 1),
     (2, 64, 16, 16, 128, 3, 2, 1),
     (2, 128, 15, 15, 256, 1, 2, 0),
-    (3, 32, 7, 7, 96, 3, 1, 1),
+    (3, 64, 7, 7, 192, 3, 1, 1),
     (2, 3, 32, 32, 64, 7, 2, 3),   # stem (C padded to 4, S to 8)
     (1, 256, 7, 7, 512, 3, 1, 1),
 ]
@@ -65,7 +65,7 @@ def test_conv_fwd(dev, shape, dtname):
     beta = torch.zeros(K, device=dev)
     rm = torch.zeros(K, device=dev)
     rv = torch.ones(K, device=dev)
-    ops.bn_finalize(K, part.numel() // (3 * K), part, gamma, beta, rm, rv, 0.1, 1e-5, True, stats[0], stats[1],
+    ops.bn_finalize(K, ops.conv_fwd_partial_tiles(g, dt), part, gamma, beta, rm, rv, 0.1, 1e-5, True, stats[0], stats[1],
                     stats[2], stats[3])
     torch.cuda.synchronize()
     r = ref.reshape(-1, K)

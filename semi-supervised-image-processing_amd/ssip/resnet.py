@@ -224,7 +224,7 @@ class SSIPResNet(nn.Module):
         if isinstance(x, DeviceImages):
             images = x.nhwc4
             if images.dtype != self.compute_dtype:
-                raise TypeError(f"DeviceImages dtype {images.dtype} != model compute dtype {self.compute_dtype}")
+                images = images.to(self.compute_dtype)
         else:
             dev = self.conv1.weight.device
             if dev.type != "cuda":

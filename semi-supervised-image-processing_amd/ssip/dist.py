@@ -32,9 +32,12 @@ def init_from_env(backend: Optional[str] = None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("SSIP_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
+        elif torch.cuda.is_available():
+            # gloo rehearsal of the DP path (several ranks may share one device)
+            torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
 
@@ -118,3 +121,33 @@ def strided_indices(indices: List[int], rank: int, world: int) -> List[int]:
     """Rank-stride a global sample stream (the WeightedRandomSampler draw is
     generated identically on every rank from the same seed)."""
     return list(indices[rank::world])
+
+
+def gather_objects(local: list, group=None) -> list:
+    """Concatenate per-rank Python lists in rank order (pseudo-label tuples,
+    evaluation records) — the shards come from `shard_range`, so the result
+    equals the single-process order."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return list(local)
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, list(local), group=group)
+    out = []
+    for p in parts:
+        out.extend(p)
+    return out
+
+
+def gather_rows(local: torch.Tensor, group=None) -> torch.Tensor:
+    """Concatenate per-rank [n_r, D] tensors (n_r may differ) in rank order."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return local
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.shape[0]], device=local.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    m = int(max(int(x) for x in ns))
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return torch.cat([b[: int(k)] for b, k in zip(bufs, ns)], 0)

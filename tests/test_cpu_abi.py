@@ -28,3 +28,10 @@ def test_argument_errors_surface_as_status_codes():
     rc = lib.ssip_conv_fwd(d, 0, None, None, None, None, None)
     assert rc == -1
     assert b"multiple of 32" in lib.ssip_last_error()
+
+
+def test_product_never_imports_the_oracle():
+    pkg = ROOT / "semi-supervised-image-processing_amd"
+    for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.cpp")):
+        txt = f.read_text()
+        assert "import oracle" not in txt and "from oracle" not in txt, f

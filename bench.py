@@ -141,7 +141,7 @@ def main():
                                                                                         + GFLOP_PER_IMG_TRAIN), 1)},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": None,
-                         "kernel": "conv_gemm_kernel (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
+                         "kernel": "conv_glds_kernel + conv_gemm_kernel (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
                                    f"in {conv_ms:.3f} ms"},
             "cpu_baseline": cpu,

@@ -194,6 +194,161 @@ struct Smem {
 };
 
 // ---------------------------------------------------------------------------
+// shared epilogue: WGRAD -> fp32 slab; FWD/DGRAD -> LDS-staged 16-B stores
+// (+ residual-gradient add for DGRAD, + BN partial statistics for FWD)
+// ---------------------------------------------------------------------------
+template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
+__device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
+                                                   int n0, int tm) {
+  constexpr int NT = 64 * WMW * WNW;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int rbase = wm * WTM + (lane >> 4) * 4;
+  const int cbase = wn * WTN + (lane & 15);
+  if constexpr (MODE == MODE_WGRAD) {
+    float* slab = static_cast<float*>(a.out) + (long)blockIdx.y * a.M * a.Ng;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + cbase + j * 16;
+        if (n >= a.Ng) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + rbase + i * 16 + e;
+          if (m < a.M) slab[(long)m * a.Ng + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+
+  // stage the tile through LDS (main loop finished: the staging buffers are free)
+  constexpr int EROW = BN * (int)sizeof(T) + 16;  // padded row (bytes)
+  {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = rbase + i * 16 + e;
+          const int col = cbase + j * 16;
+          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) = from_f32<T>(acc[i][j][e]);
+        }
+  }
+  __syncthreads();
+  {
+    // each thread moves 8-element chunks: BN/8 chunks per row
+    constexpr int CPR = BN / 8;
+    T* Out = static_cast<T*>(a.out);   // may alias Add (in-place residual-gradient add)
+    const T* Add = static_cast<const T*>(a.add);
+    for (int id = tid; id < BM * CPR; id += NT) {
+      const int row = id / CPR, ch = id % CPR;
+      const int m = m0 + row, n = n0 + ch * 8;
+      if (m >= a.M || n >= a.Ng) continue;
+      Vec8<T> v;
+      const char* src = smem + row * EROW + ch * 8 * (int)sizeof(T);
+      if constexpr (sizeof(T) == 2) {
+        v.v = *reinterpret_cast<const i32x4*>(src);
+      } else {
+        reinterpret_cast<Vec8<float>&>(v).v0 = reinterpret_cast<const i32x4*>(src)[0];
+        reinterpret_cast<Vec8<float>&>(v).v1 = reinterpret_cast<const i32x4*>(src)[1];
+      }
+      if constexpr (MODE == MODE_DGRAD) {
+        if (Add) {
+          // the unrounded accumulator would be better; the LDS copy is already in T
+          Vec8<T> r;
+          r.load(Add + (long)m * a.Ng + n);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v.set(j, v.get(j) + r.get(j));
+        }
+      }
+      v.store(Out + (long)m * a.Ng + n);
+    }
+  }
+
+  if constexpr (MODE == MODE_FWD) {
+    if (a.partial == nullptr) return;
+    __syncthreads();
+    // BatchNorm partial statistics over this tile's valid rows (from fp32 accumulators).
+    float* red = reinterpret_cast<float*>(smem);  // [WMW][BN]
+    float* mean_t = red + WMW * BN;               // [BN]
+    const int cnt = min(BM, a.M - m0);
+    float s[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = rbase + i * 16 + e;
+          t += (row < cnt) ? acc[i][j][e] : 0.f;
+        }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      s[j] = t;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = s[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+      mean_t[c] = t / (float)cnt;
+    }
+    __syncthreads();
+    float q2[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const float mu = mean_t[cbase + j * 16];
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = rbase + i * 16 + e;
+          const float d = acc[i][j][e] - mu;
+          t += (row < cnt) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      q2[j] = t;
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = q2[j];
+    }
+    __syncthreads();
+    const int tiles_m = gridDim.x / a.tiles_n;
+    for (int c = tid; c < BN; c += NT) {
+      const int n = n0 + c;
+      if (n < a.Ng) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+        float* rec = a.partial + ((long)n * tiles_m + tm) * 3;  // [C][tiles][3]
+        rec[0] = (float)cnt;
+        rec[1] = mean_t[c] * (float)cnt;
+        rec[2] = t;
+      }
+    }
+  }
+}
+
+template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
+                                              int tm) {
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm);
+}
+
+// ---------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, bool CONV1>
@@ -456,142 +611,251 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_gemm_kernel(const ConvArg
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  const int rbase = wm * WTM + (lane >> 4) * 4;
-  const int cbase = wn * WTN + (lane & 15);
-  if constexpr (MODE == MODE_WGRAD) {
-    float* slab = static_cast<float*>(a.out) + (long)blockIdx.y * a.M * a.Ng;
+  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 fast path: LDS-DMA (global_load_lds_dwordx4) 3-stage ring.
+// Each wave-instruction moves 64 x 16 B = 1 KiB straight into LDS (no VGPR
+// staging, no ds_write); the XOR swizzle is applied to the per-lane SOURCE
+// chunk so the LDS image is the same one the register-staged kernel builds.
+// Padded / out-of-range taps read a 16-byte zero block.  Prefetch distance
+// 2: the loop waits with a counted vmcnt (one stage left in flight) and a
+// raw s_barrier, never vmcnt(0) until the last step.
+// ---------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) int g_zero16[4];
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_block) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_block, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE>
+__global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArgs a) {
+  typedef __bf16 T;
+  constexpr int NW = WMW * WNW, BK = 64;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr bool WG = (MODE == MODE_WGRAD);
+  constexpr int A_BYTES = WG ? BK * BM * 2 : BM * 128;
+  constexpr int B_BYTES = WG ? BK * BN * 2 : BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "2 or 3 LDS stages");
+  constexpr int IA = A_BYTES / 1024, IB = B_BYTES / 1024;
+  constexpr int LA = IA / NW, LB = IB / NW;
+  constexpr int L = LA + LB;
+  static_assert(IA % NW == 0 && IB % NW == 0 && LA >= 1 && LB >= 1, "bad glds tile");
+  static_assert(FM >= 1 && FN >= 1, "bad wave tile");
+  constexpr int EPI = WG ? 0 : BM * (BN * 2 + 16);
+  constexpr int SMEM = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int tn = blockIdx.x % a.tiles_n;
+  const int tm = blockIdx.x / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const T* __restrict__ Ag = static_cast<const T*>(a.A);
+  const T* __restrict__ Bg = static_cast<const T*>(a.B);
+
+  // ---------------- per-lane source state ----------------
+  // FWD/DGRAD: instruction j = wave + NW*t covers k-tile rows 8j..8j+7;
+  //   lane -> row 8j + lane/8, LDS slot lane%8 holds logical chunk (lane%8) ^ ((row>>1)&7)
+  // WGRAD: rows of CPR = cols/8 chunks; instruction j covers 64/CPR rows.
+  int a_base[LA], a_h[LA], a_w[LA], a_c[LA];
+  bool a_ok[LA];
+  const T* b_ptr[LB];
+  int b_r[LB], b_s[LB], b_c[LB], b_row[LB];
+  bool b_ok[LB];
+  int kr = 0, ks_ = 0, kcb = 0;
+  const int Cred = (MODE == MODE_FWD) ? a.C : a.K;
+  long mstart = 0, mend = 0;
+
+  if constexpr (!WG) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + cbase + j * 16;
-        if (n >= a.Ng) continue;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + rbase + i * 16 + e;
-          if (m < a.M) slab[(long)m * a.Ng + n] = acc[i][j][e];
-        }
+    for (int t = 0; t < LA; ++t) {
+      const int row = 8 * (wave + NW * t) + (lane >> 3);
+      a_c[t] = (lane & 7) ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      a_ok[t] = m < a.M;
+      const int mm = a_ok[t] ? m : 0;
+      if constexpr (MODE == MODE_FWD) {
+        const int n = fdiv(mm, a.div_pq);
+        const int rem = mm - n * a.P * a.Q;
+        const int p = fdiv(rem, a.div_q);
+        const int q = rem - p * a.Q;
+        a_base[t] = n * a.H * a.W;
+        a_h[t] = p * a.stride - a.pad;
+        a_w[t] = q * a.stride - a.pad;
+      } else {
+        const int n = fdiv(mm, a.div_hw);
+        const int rem = mm - n * a.H * a.W;
+        const int h = fdiv(rem, a.div_w);
+        const int w = rem - h * a.W;
+        a_base[t] = n * a.P * a.Q;
+        a_h[t] = h + a.pad;
+        a_w[t] = w + a.pad;
       }
-    return;
+    }
+#pragma unroll
+    for (int t = 0; t < LB; ++t) {
+      const int row = 8 * (wave + NW * t) + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int n = n0 + row;
+      b_ok[t] = n < a.Ng;
+      b_ptr[t] = Bg + (long)(b_ok[t] ? n : 0) * a.Kg + c * 8;
+    }
+  } else {
+    mstart = (long)blockIdx.y * a.ksteps * BK;
+    mend = mstart + (long)a.ksteps * BK;
+    if (mend > a.Mred) mend = a.Mred;
+    constexpr int CPA = BM / 8, RPA = 64 / CPA;
+    constexpr int CPB = BN / 8, RPB = 64 / CPB;
+#pragma unroll
+    for (int t = 0; t < LA; ++t) {
+      const int row = RPA * (wave + NW * t) + lane / CPA;
+      const int lc = (lane % CPA) ^ (MTile<T, BM>::swz(row) >> 1);
+      a_h[t] = row;                       // m-row within the k-step
+      a_c[t] = m0 + lc * 8;               // output-channel column
+      a_ok[t] = a_c[t] < a.K;
+    }
+#pragma unroll
+    for (int t = 0; t < LB; ++t) {
+      const int row = RPB * (wave + NW * t) + lane / CPB;
+      const int lc = (lane % CPB) ^ (MTile<T, BN>::swz(row) >> 1);
+      const int col = n0 + lc * 8;
+      b_row[t] = row;
+      b_ok[t] = col < a.Ng;
+      const int cc = b_ok[t] ? col : 0;
+      const int rs = cc / a.C;
+      b_c[t] = cc - rs * a.C;
+      b_r[t] = rs / a.S;
+      b_s[t] = rs - b_r[t] * a.S;
+    }
   }
 
-  // stage the tile through LDS (main loop finished: the staging buffers are free)
-  constexpr int EROW = BN * (int)sizeof(T) + 16;  // padded row (bytes)
-  {
+  auto issue = [&](int ks, int stage) {
+    char* As = smem + stage * STAGE;
+    char* Bs = As + A_BYTES;
+    if constexpr (MODE == MODE_FWD) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int t = 0; t < LA; ++t) {
+        const int hin = a_h[t] + kr, win = a_w[t] + ks_;
+        const bool ok = a_ok[t] && hin >= 0 && hin < a.H && win >= 0 && win < a.W;
+        const T* src = ok ? Ag + ((long)(a_base[t] + hin * a.W + win)) * a.C + kcb + a_c[t] * 8
+                          : reinterpret_cast<const T*>(g_zero16);
+        glds16(src, As + (wave + NW * t) * 1024);
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = rbase + i * 16 + e;
-          const int col = cbase + j * 16;
-          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) = from_f32<T>(acc[i][j][e]);
+      for (int t = 0; t < LA; ++t) {
+        const int hp = a_h[t] - kr, wp = a_w[t] - ks_;
+        int p = hp, q = wp;
+        bool ok = a_ok[t] && hp >= 0 && wp >= 0;
+        if (a.stride != 1) {
+          ok = ok && ((hp | wp) & (a.stride - 1)) == 0;
+          p = hp >> (a.stride >> 1);
+          q = wp >> (a.stride >> 1);
         }
+        ok = ok && p < a.P && q < a.Q;
+        const T* src = ok ? Ag + ((long)(a_base[t] + p * a.Q + q)) * a.K + kcb + a_c[t] * 8
+                          : reinterpret_cast<const T*>(g_zero16);
+        glds16(src, As + (wave + NW * t) * 1024);
+      }
+    }
+    if constexpr (!WG) {
+#pragma unroll
+      for (int t = 0; t < LB; ++t) {
+        const T* src = b_ok[t] ? b_ptr[t] + ks * BK : reinterpret_cast<const T*>(g_zero16);
+        glds16(src, Bs + (wave + NW * t) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < LA; ++t) {
+        const long m = mstart + (long)ks * BK + a_h[t];
+        const bool ok = a_ok[t] && m < mend;
+        const T* src = ok ? Ag + m * (long)a.K + a_c[t] : reinterpret_cast<const T*>(g_zero16);
+        glds16(src, As + (wave + NW * t) * 1024);
+      }
+#pragma unroll
+      for (int t = 0; t < LB; ++t) {
+        const long m = mstart + (long)ks * BK + b_row[t];
+        const bool mok = b_ok[t] && m < mend;
+        const int mm = mok ? (int)m : 0;
+        const int n = fdiv(mm, a.div_pq);
+        const int rem = mm - n * a.P * a.Q;
+        const int p = fdiv(rem, a.div_q);
+        const int q = rem - p * a.Q;
+        const int hin = p * a.stride - a.pad + b_r[t];
+        const int win = q * a.stride - a.pad + b_s[t];
+        const bool ok = mok && hin >= 0 && hin < a.H && win >= 0 && win < a.W;
+        const T* src = ok ? Bg + ((long)((n * a.H + hin) * a.W + win)) * a.C + b_c[t]
+                          : reinterpret_cast<const T*>(g_zero16);
+        glds16(src, Bs + (wave + NW * t) * 1024);
+      }
+    }
+    if constexpr (!WG) {
+      kcb += BK;
+      if (kcb >= Cred) {
+        kcb = 0;
+        if (++ks_ >= a.S) { ks_ = 0; ++kr; }
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  int nsteps = a.ksteps;
+  if constexpr (WG) {
+    const long rem = mend - mstart;
+    nsteps = rem > 0 ? (int)((rem + BK - 1) / BK) : 0;
+  }
+  // NSTAGE-deep ring, NSTAGE-1 k-steps in flight.  Step ks: retire stage ks
+  // with a counted vmcnt (the later in-flight steps stay outstanding across
+  // the raw barrier), then refill the slot every wave finished reading in
+  // step ks-1.
+  if (nsteps > 0) issue(0, 0);
+  if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
+  int stage = 0;
+  for (int ks = 0; ks < nsteps; ++ks) {
+    if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
+    if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
+    const char* As = smem + stage * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      Frag<T> fa[FM], fb[FN];
+      if constexpr (!WG) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) read_kfrag(fa[i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) read_kfrag(fb[j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, h);
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[i], As, wm * WTM + i * 16, lane, h);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[j], Bs, wn * WTN + j * 16, lane, h);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
+    }
+    stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();
-  {
-    // each thread moves 8-element chunks: BN/8 chunks per row
-    constexpr int CPR = BN / 8;
-    T* Out = static_cast<T*>(a.out);   // may alias Add (in-place residual-gradient add)
-    const T* Add = static_cast<const T*>(a.add);
-    for (int id = tid; id < BM * CPR; id += NT) {
-      const int row = id / CPR, ch = id % CPR;
-      const int m = m0 + row, n = n0 + ch * 8;
-      if (m >= a.M || n >= a.Ng) continue;
-      Vec8<T> v;
-      const char* src = smem + row * EROW + ch * 8 * (int)sizeof(T);
-      if constexpr (sizeof(T) == 2) {
-        v.v = *reinterpret_cast<const i32x4*>(src);
-      } else {
-        reinterpret_cast<Vec8<float>&>(v).v0 = reinterpret_cast<const i32x4*>(src)[0];
-        reinterpret_cast<Vec8<float>&>(v).v1 = reinterpret_cast<const i32x4*>(src)[1];
-      }
-      if constexpr (MODE == MODE_DGRAD) {
-        if (Add) {
-          // the unrounded accumulator would be better; the LDS copy is already in T
-          Vec8<T> r;
-          r.load(Add + (long)m * a.Ng + n);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v.set(j, v.get(j) + r.get(j));
-        }
-      }
-      v.store(Out + (long)m * a.Ng + n);
-    }
-  }
-
-  if constexpr (MODE == MODE_FWD) {
-    if (a.partial == nullptr) return;
-    __syncthreads();
-    // BatchNorm partial statistics over this tile's valid rows (from fp32 accumulators).
-    float* red = reinterpret_cast<float*>(smem);  // [WMW][BN]
-    float* mean_t = red + WMW * BN;               // [BN]
-    const int cnt = min(BM, a.M - m0);
-    float s[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = rbase + i * 16 + e;
-          t += (row < cnt) ? acc[i][j][e] : 0.f;
-        }
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      s[j] = t;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = s[j];
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-      mean_t[c] = t / (float)cnt;
-    }
-    __syncthreads();
-    float q2[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const float mu = mean_t[cbase + j * 16];
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = rbase + i * 16 + e;
-          const float d = acc[i][j][e] - mu;
-          t += (row < cnt) ? d * d : 0.f;
-        }
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      q2[j] = t;
-    }
-    __syncthreads();
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = q2[j];
-    }
-    __syncthreads();
-    const int tiles_m = gridDim.x / a.tiles_n;
-    for (int c = tid; c < BN; c += NT) {
-      const int n = n0 + c;
-      if (n < a.Ng) {
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-        float* rec = a.partial + ((long)n * tiles_m + tm) * 3;  // [C][tiles][3]
-        rec[0] = (float)cnt;
-        rec[1] = mean_t[c] * (float)cnt;
-        rec[2] = t;
-      }
-    }
-  }
+  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -638,6 +902,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
 struct Plan {
   int mode;
   int bm, bn, wmw, wnw;
+  int stages;  // 2/3: LDS-DMA ring kernel (bf16); 0: register-staged kernel
   bool conv1;
   ConvArgs args;
   dim3 grid;
@@ -668,6 +933,47 @@ static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
   } else {
     pl.bm = 128; pl.bn = bn; pl.wmw = 2; pl.wnw = 2;
   }
+}
+
+static bool glds_has(int mode, int bm, int bn, int wm, int wn, int st);
+
+// Default LDS-DMA configuration for a bf16 GEMM view (M x Ng, reduction Kg).
+// Chosen from tools/tune_conv.py over the ResNet-18 train-step shapes
+// (profiles/r1_conv_tune.txt): two LDS stages and 8-16 waves per workgroup
+// beat deeper rings at one workgroup per CU on every shape; 2-3 workgroups
+// per CU hide each other's barriers and epilogues.
+static void choose_glds(int mode, const ConvArgs& a, Plan& pl) {
+  pl.stages = 2;
+  if (mode == MODE_WGRAD) {
+    if (a.M % 128 == 0) { pl.bm = 128; pl.bn = 128; pl.wmw = 4; pl.wnw = 4; }
+    else { pl.bm = 64; pl.bn = 128; pl.wmw = 2; pl.wnw = 4; }
+    return;
+  }
+  pl.bm = 128; pl.wmw = 4; pl.wnw = 2;
+  pl.bn = (a.Ng % 128 == 0) ? 128 : 64;
+}
+
+// Tuning override: SSIP_CONV_FORCE="<f|d|w>,bm,bn,waves_m,waves_n,stages"
+// (stages 0 = register-staged kernel) applies to the named pass only.
+static int apply_force(int mode, int elem_bytes, Plan& pl) {
+  const char* e = getenv("SSIP_CONV_FORCE");
+  if (!e || !e[0]) return SSIP_OK;
+  const char want = mode == MODE_FWD ? 'f' : mode == MODE_DGRAD ? 'd' : 'w';
+  if (e[0] != want || pl.conv1) return SSIP_OK;
+  int bm, bn, wm, wn, st;
+  SSIP_REQUIRE(sscanf(e + 1, ",%d,%d,%d,%d,%d", &bm, &bn, &wm, &wn, &st) == 5, SSIP_ERR_ARG,
+               "bad SSIP_CONV_FORCE '%s'", e);
+  if (st > 0) {
+    SSIP_REQUIRE(elem_bytes == 2 && glds_has(mode, bm, bn, wm, wn, st), SSIP_ERR_ARG,
+                 "SSIP_CONV_FORCE: no LDS-DMA kernel %s", e);
+  } else {
+    const bool ok = mode == MODE_WGRAD ? (wm == 2 && wn == 2 && (bm == 128 || bm == 64))
+                                       : ((bm == 256 && wm == 4 && wn == 2 && elem_bytes == 2) ||
+                                          (bm == 128 && wm == 2 && wn == 2));
+    SSIP_REQUIRE(ok && (bn == 128 || bn == 64), SSIP_ERR_ARG, "SSIP_CONV_FORCE: no register-staged kernel %s", e);
+  }
+  pl.bm = bm; pl.bn = bn; pl.wmw = wm; pl.wnw = wn; pl.stages = st;
+  return SSIP_OK;
 }
 
 static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl) {
@@ -706,6 +1012,11 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
     pl.bm = (d->K % 128 == 0) ? 128 : 64;
     pl.bn = 128;
     if (a.Ng % 128 != 0 && a.Ng % 64 == 0 && pl.bm == 128) pl.bn = 64;
+  }
+  pl.stages = 0;
+  if (elem_bytes == 2 && !pl.conv1) choose_glds(mode, a, pl);
+  if (int rc = apply_force(mode, elem_bytes, pl)) return rc;
+  if (mode == MODE_WGRAD) {
     const int tiles = ceil_div(a.M, pl.bm) * ceil_div(a.Ng, pl.bn);
     const int total_ks = ceil_div(a.Mred, BK);
     // ~1024 blocks (4 per CU), slab <= 64 MiB (stays in the Infinity Cache),
@@ -727,8 +1038,53 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   return SSIP_OK;
 }
 
+// LDS-DMA ring kernel configurations (bm, bn, waves_m, waves_n, stages).
+#define SSIP_GLDS_FD(X)                                                                                      \
+  X(256, 128, 4, 2, 3) X(256, 128, 4, 2, 2) X(256, 64, 4, 1, 2) X(256, 64, 4, 1, 3) X(256, 64, 4, 2, 2)        \
+  X(256, 64, 4, 2, 3) X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 2, 3)      \
+  X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
+  X(256, 128, 4, 4, 2)
+#define SSIP_GLDS_WG(X)                                                                                      \
+  X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
+  X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
+  X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
+  X(64, 128, 1, 8, 2)
+
+static bool glds_has(int mode, int bm, int bn, int wm, int wn, int st) {
+#define SSIP_GLDS_EQ(BM_, BN_, WM_, WN_, ST_) \
+  if (bm == BM_ && bn == BN_ && wm == WM_ && wn == WN_ && st == ST_) return true;
+  if (mode == MODE_WGRAD) {
+    SSIP_GLDS_WG(SSIP_GLDS_EQ)
+  } else {
+    SSIP_GLDS_FD(SSIP_GLDS_EQ)
+  }
+#undef SSIP_GLDS_EQ
+  return false;
+}
+
+template <int MODE>
+static int launch_glds(const Plan& pl, hipStream_t st) {
+#define SSIP_GLDS_GO(BM_, BN_, WM_, WN_, ST_)                                                                 \
+  if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
+                       st, pl.args);                                                                          \
+    return ::ssip::check_launch("conv_glds");                                                                 \
+  }
+  if constexpr (MODE == MODE_WGRAD) {
+    SSIP_GLDS_WG(SSIP_GLDS_GO)
+  } else {
+    SSIP_GLDS_FD(SSIP_GLDS_GO)
+  }
+#undef SSIP_GLDS_GO
+  ::ssip::set_error("no LDS-DMA conv kernel for %dx%d/%dx%d/%d", pl.bm, pl.bn, pl.wmw, pl.wnw, pl.stages);
+  return SSIP_ERR_ARG;
+}
+
 template <int MODE, typename T>
 static int launch_conv(const Plan& pl, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (pl.stages > 0) return launch_glds<MODE>(pl, st);
+  }
 #define SSIP_LAUNCH(BM_, BN_, WM_, WN_, C1_)                                                                  \
   {                                                                                                           \
     hipLaunchKernelGGL((conv_gemm_kernel<MODE, T, BM_, BN_, WM_, WN_, C1_>), pl.grid, dim3(64 * WM_ * WN_), 0, \

@@ -5,9 +5,10 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 rows = list(csv.DictReader(open(path)))
 fam = collections.defaultdict(lambda: [0.0, 0])
 def family(n):
-    if 'conv_gemm_kernel' in n:
-        mode = n.split('conv_gemm_kernelILi')[1][0]
-        return {'0': 'conv_fwd', '1': 'conv_dgrad', '2': 'conv_wgrad'}[mode]
+    for k in ('conv_gemm_kernelILi', 'conv_glds_kernelILi', 'conv_glds_kernel<'):
+        if k in n:
+            mode = n.split(k)[1][0]
+            return {'0': 'conv_fwd', '1': 'conv_dgrad', '2': 'conv_wgrad'}[mode]
     for k in ['wgrad_reduce', 'bn_apply', 'bn_bwd_apply', 'bn_bwd_reduce', 'bn_bwd_finalize', 'bn_finalize',
               'maxpool_fwd', 'maxpool_bwd', 'augment', 'resize_h', 'weight_prep', 'adamw', 'avgpool_fc_fwd',
               'avgpool_fc_bwd', 'fc_bwd_weight', 'semi_loss', 'cross_entropy', 'nchw_to_nhwc']:

@@ -159,6 +159,16 @@ int ssip_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float
 /* w_kcrs (fp32 torchvision layout) -> w_krsc [K][R][Sp][Cp] and/or w_crsk [Cp][R][Sp][K] in dtype */
 int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, const float* w_kcrs, void* w_krsc,
                      void* w_crsk, void* stream);
+/* Batched form: every stale conv weight of a model in one launch (per step).
+ * krsc or crsk may be NULL per item; count <= SSIP_WPREP_MAX per call. */
+#define SSIP_WPREP_MAX 32
+typedef struct ssip_wprep {
+  int K, C, R, S, Cp, Sp;
+  const float* w_kcrs;
+  void* w_krsc;
+  void* w_crsk;
+} ssip_wprep;
+int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* items, void* stream);
 
 #ifdef __cplusplus
 }

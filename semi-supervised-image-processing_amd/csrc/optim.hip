@@ -51,6 +51,54 @@ __global__ void weight_prep_kernel(int K, int C, int R, int S, int Cp, int Sp, c
   }
 }
 
+// Batched preparation: one workgroup per (item, 64-k tile, 64-c tile, r, s);
+// the 64x64 K x C slice is staged through LDS so both outputs are written as
+// contiguous rows (KRSC rows run over c, CRSK rows over k).  One slice per
+// workgroup keeps every load independent (a per-workgroup (r, s) loop
+// serialises ~R*S HBM round trips: 0.36 ms for ResNet-18).
+struct WprepTable {
+  ssip_wprep it[SSIP_WPREP_MAX];
+  int tile_start[SSIP_WPREP_MAX + 1];
+  int count;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) weight_prep_batch_kernel(const WprepTable tab) {
+  __shared__ float tile[64][65];
+  int b = blockIdx.x, idx = 0;
+  while (idx + 1 < tab.count && b >= tab.tile_start[idx + 1]) ++idx;
+  const ssip_wprep& e = tab.it[idx];
+  b -= tab.tile_start[idx];
+  const int rs = b % (e.R * e.Sp);
+  b /= e.R * e.Sp;
+  const int r = rs / e.Sp, s = rs - r * e.Sp;
+  const int ctiles = (e.Cp + 63) / 64;
+  const int k0 = (b / ctiles) * 64, c0 = (b % ctiles) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  T* krsc = static_cast<T*>(e.w_krsc);
+  T* crsk = static_cast<T*>(e.w_crsk);
+#pragma unroll 4
+  for (int kk = ty; kk < 64; kk += 4) {
+    const int k = k0 + kk, c = c0 + tx;
+    float v = 0.f;
+    if (k < e.K && c < e.C && s < e.S) v = e.w_kcrs[(((long)k * e.C + c) * e.R + r) * e.S + s];
+    tile[kk][tx] = v;
+  }
+  __syncthreads();
+  if (krsc) {
+    for (int kk = ty; kk < 64; kk += 4) {
+      const int k = k0 + kk, c = c0 + tx;
+      if (k < e.K && c < e.Cp) krsc[(((long)k * e.R + r) * e.Sp + s) * e.Cp + c] = from_f32<T>(tile[kk][tx]);
+    }
+  }
+  if (crsk) {
+    for (int cc = ty; cc < 64; cc += 4) {
+      const int c = c0 + cc, k = k0 + tx;
+      if (k < e.K && c < e.Cp) crsk[(((long)c * e.R + r) * e.Sp + s) * e.K + k] = from_f32<T>(tile[tx][cc]);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -85,3 +133,27 @@ int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, cons
 }
 
 }  // extern "C"
+
+extern "C" int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* items, void* stream) {
+  SSIP_REQUIRE(count >= 0 && count <= SSIP_WPREP_MAX && (count == 0 || items), SSIP_ERR_ARG,
+               "ssip_weight_prep_batch: count must be 0..%d", SSIP_WPREP_MAX);
+  if (count == 0) return SSIP_OK;
+  WprepTable tab;
+  memset(&tab, 0, sizeof(tab));
+  tab.count = count;
+  int tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    const ssip_wprep& e = items[i];
+    SSIP_REQUIRE(e.K > 0 && e.C > 0 && e.R > 0 && e.S > 0 && e.Cp >= e.C && e.Sp >= e.S && e.w_kcrs &&
+                     (e.w_krsc || e.w_crsk),
+                 SSIP_ERR_ARG, "ssip_weight_prep_batch: bad item %d", i);
+    tab.it[i] = e;
+    tab.tile_start[i] = tiles;
+    tiles += ((e.K + 63) / 64) * ((e.Cp + 63) / 64) * e.R * e.Sp;
+  }
+  tab.tile_start[count] = tiles;
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(weight_prep_batch_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, tab);
+  });
+  return ::ssip::check_launch("weight_prep_batch");
+}

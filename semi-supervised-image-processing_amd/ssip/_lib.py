@@ -27,6 +27,14 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("N", "H", "W", "C", "K", "R", "S", "stride", "pad", "P", "Q")]
 
 
+WPREP_MAX = 32
+
+
+class WPrep(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("K", "C", "R", "S", "Cp", "Sp")] + [
+        ("w_kcrs", ctypes.c_void_p), ("w_krsc", ctypes.c_void_p), ("w_crsk", ctypes.c_void_p)]
+
+
 class AugParam(ctypes.Structure):
     _fields_ = [
         ("flip", ctypes.c_int32),
@@ -81,6 +89,7 @@ _SIGS = {
     "ssip_nchw_to_nhwc": (_c_int, [_c_int] * 6 + [_vp, _vp, _vp]),
     "ssip_adamw": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_f, _vp]),
     "ssip_weight_prep": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp, _vp]),
+    "ssip_weight_prep_batch": (_c_int, [_c_int, _c_int, ctypes.POINTER(WPrep), _vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

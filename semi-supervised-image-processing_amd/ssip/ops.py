@@ -167,6 +167,22 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
     call(*args)
 
 
+def weight_prep_batch(items, dtype: torch.dtype) -> None:
+    """items: [(w_kcrs fp32, Cp, Sp, krsc or None, crsk or None)] -> one launch per 32."""
+    for i in range(0, len(items), _lib.WPREP_MAX):
+        chunk = items[i:i + _lib.WPREP_MAX]
+        arr = (_lib.WPrep * len(chunk))()
+        for j, (w, Cp, Sp, krsc, crsk) in enumerate(chunk):
+            assert w.dtype == torch.float32 and w.is_contiguous()
+            K, C, R, S = w.shape
+            if krsc is not None:
+                assert krsc.dtype == dtype and krsc.numel() == K * R * Sp * Cp
+            if crsk is not None:
+                assert crsk.dtype == dtype and crsk.numel() == K * R * Sp * Cp
+            arr[j] = _lib.WPrep(K, C, R, S, Cp, Sp, _p(w), _p(krsc), _p(crsk))
+        call("ssip_weight_prep_batch", _DT[dtype], len(chunk), arr, stream_ptr())
+
+
 def weight_prep(w: torch.Tensor, dtype: torch.dtype, Cp: int, Sp: int, krsc: Optional[torch.Tensor],
                 crsk: Optional[torch.Tensor]) -> None:
     K, C, R, S = w.shape

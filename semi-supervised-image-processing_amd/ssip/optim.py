@@ -14,6 +14,7 @@ from __future__ import annotations
 from typing import Dict, Iterable, List, Tuple
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import ops
 
@@ -87,4 +88,7 @@ class AdamW(torch.optim.Optimizer):
                 st = self.state[p]
                 ops.adamw(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
                           group["eps"], group["weight_decay"], int(st["step"].item()), grad_scale)
+            # the kernels write through raw pointers: tell torch (and the
+            # model's compute-dtype weight cache) that these tensors changed
+            increment_version(params)
         return loss

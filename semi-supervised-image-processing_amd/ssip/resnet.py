@@ -174,7 +174,8 @@ class SSIPResNet(nn.Module):
                 nn.init.constant_(m.bias, 0)
         self.compute_dtype = _DTYPES[dtype]
         self.bn_update_running = True   # may be switched off for no-update batch-stat passes
-        self._prep: Dict[Tuple[int, torch.dtype], Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
+        # (id(conv), dtype) -> [krsc, crsk or None, weight version they were made from]
+        self._prep: Dict[Tuple[int, torch.dtype], list] = {}
         self._arena = None
         self.embedding_only = False
 
@@ -274,19 +275,38 @@ def _geom(conv: nn.Conv2d, N: int, H: int, W: int) -> ConvGeom:
                     stride=conv.stride[0], pad=conv.padding[0], c_real=C, s_real=S)
 
 
-def _prepped(model: SSIPResNet, conv: nn.Conv2d, g: ConvGeom, need_t: bool):
+def _prepare_weights(model: SSIPResNet, need_t: bool) -> None:
+    """Refresh the compute-dtype KRSC (forward) and CRSK (data-gradient)
+    copies of every conv weight whose fp32 master changed since the last
+    refresh (torch version counter; ssip.optim.AdamW bumps it), in one
+    batched launch — once per optimizer step, not once per forward."""
     dt = model.compute_dtype
-    key = (id(conv), dt)
-    ent = model._prep.get(key)
-    w = conv.weight
-    if ent is None or (need_t and ent[1] is None):
-        krsc = torch.empty((g.K, g.R, g.S, g.C), device=w.device, dtype=dt)
-        crsk = torch.empty((g.C, g.R, g.S, g.K), device=w.device, dtype=dt) if need_t else None
-        ent = (krsc, crsk)
-        model._prep[key] = ent
-    # weights change every optimizer step: re-prepare every forward (one
-    # HBM-bound pass over 44.7 MB of fp32 masters for ResNet-18)
-    ops.weight_prep(w.detach(), dt, g.C, g.S, ent[0], ent[1] if need_t else None)
+    items = []
+    for conv in model.modules():
+        if not isinstance(conv, nn.Conv2d):
+            continue
+        w = conv.weight
+        key = (id(conv), dt)
+        ent = model._prep.get(key)
+        if ent is not None and ent[2] == w._version and (ent[1] is not None or not need_t):
+            continue
+        g = _geom(conv, 1, 1, 1)
+        if ent is None or (need_t and ent[1] is None):
+            krsc = torch.empty((g.K, g.R, g.S, g.C), device=w.device, dtype=dt)
+            crsk = torch.empty((g.C, g.R, g.S, g.K), device=w.device, dtype=dt) if need_t else None
+        else:
+            krsc, crsk = ent[0], ent[1]
+        model._prep[key] = [krsc, crsk, w._version]
+        items.append((w.detach(), g.C, g.S, krsc, crsk))
+    if items:
+        ops.weight_prep_batch(items, dt)
+
+
+def _prepped(model: SSIPResNet, conv: nn.Conv2d, g: ConvGeom, need_t: bool):
+    ent = model._prep.get((id(conv), model.compute_dtype))
+    if ent is None or ent[2] != conv.weight._version or (need_t and ent[1] is None):
+        _prepare_weights(model, need_t)
+        ent = model._prep[(id(conv), model.compute_dtype)]
     return ent
 
 
@@ -294,7 +314,7 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
              update_running: bool) -> _ConvRec:
     g = _geom(conv, N, H, W)
     dt = model.compute_dtype
-    krsc, _ = _prepped(model, conv, g, need_t=save)
+    krsc = _prepped(model, conv, g, need_t=save)[0]
     y = torch.empty((N, g.P, g.Q, g.K), device=x.device, dtype=dt)
     stats = torch.empty((4, g.K), device=x.device, dtype=torch.float32)
     if train:
@@ -317,6 +337,7 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool) -
     upd = train and model.bn_update_running
     sv = _Saved(dtype=dt, N=N)
     dev = images.device
+    _prepare_weights(model, need_t=save)
     # stem: conv 7x7/2 -> BN -> ReLU -> maxpool 3x3/2
     rec = _conv_bn(model, model.conv1, model.bn1, images, N, H, W, train, save, upd)
     g = rec.geom
@@ -477,7 +498,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
 
     def conv_dgrad(rec: _ConvRec, dy, out, add=None):
-        _, crsk = _prepped_t(model, rec)
+        crsk = _prepped_t(model, rec)[1]
         ops.conv_dgrad(rec.geom, dy, crsk, out, add)
 
     nblocks = len(sv.blocks)
@@ -532,11 +553,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
 
 
 def _prepped_t(model: SSIPResNet, rec: _ConvRec):
-    dt = model.compute_dtype
-    ent = model._prep.get((id(rec.conv), dt))
-    if ent is None or ent[1] is None:
-        ent = _prepped(model, rec.conv, rec.geom, need_t=True)
-    return ent
+    return _prepped(model, rec.conv, rec.geom, need_t=True)
 
 
 # ---------------------------------------------------------------------------

@@ -204,3 +204,54 @@ def test_adamw_matches_torch(dev):
         ops.adamw(p, g.to(dev), m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-2, t)
     torch.cuda.synchronize()
     assert _rel(p, ref.detach()) < 1e-6
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_weight_prep_batch_layouts(dev, dtname):
+    """Batched prep == the per-tensor layouts (exact): KRSC / CRSK, zero
+    padding of the stem (C 3->4, S 7->8), ragged K/C (not multiples of 64)."""
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    torch.manual_seed(0)
+    shapes = [(64, 3, 7, 7, 4, 8), (128, 64, 3, 3, 64, 3), (96, 40, 1, 1, 40, 1), (512, 256, 3, 3, 256, 3)]
+    items, refs = [], []
+    for K, C, R, S, Cp, Sp in shapes:
+        w = torch.randn(K, C, R, S)
+        pad = torch.zeros(K, Cp, R, Sp)
+        pad[:, :C, :, :S] = w
+        krsc_ref = pad.permute(0, 2, 3, 1).contiguous().to(dt)
+        crsk_ref = pad.permute(1, 2, 3, 0).contiguous().to(dt)
+        krsc = torch.full((K, R, Sp, Cp), float("nan"), device=dev, dtype=dt)
+        crsk = torch.full((Cp, R, Sp, K), float("nan"), device=dev, dtype=dt)
+        items.append((w.to(dev), Cp, Sp, krsc, crsk))
+        refs.append((krsc_ref, crsk_ref, krsc, crsk))
+    ops.weight_prep_batch(items, dt)
+    torch.cuda.synchronize()
+    for krsc_ref, crsk_ref, krsc, crsk in refs:
+        assert torch.equal(krsc.cpu(), krsc_ref)
+        assert torch.equal(crsk.cpu(), crsk_ref)
+
+
+def test_weight_cache_follows_optimizer(dev):
+    """The compute-dtype weight copies are refreshed after every optimizer
+    step (version counter) and reused between steps."""
+    from ssip import SSIPResNet
+    from ssip.optim import AdamW
+    torch.manual_seed(0)
+    m = SSIPResNet("resnet18", num_classes=2, dtype="fp32").to(dev)
+    arena = m.flatten_parameters()
+    x = torch.randn(2, 3, 32, 32, device=dev)
+    out = m(x)
+    key = (id(m.conv1), m.compute_dtype)
+    before = m._prep[key][0].clone()
+    out.sum().backward()
+    opt = AdamW(m.parameters(), lr=1e-2, arena=arena)
+    opt.step()
+    v = m.conv1.weight._version
+    assert m._prep[key][2] != v
+    m(x)
+    assert m._prep[key][2] == v
+    w = m.conv1.weight.detach()
+    exp = torch.zeros(64, 7, 8, 4, device=dev)
+    exp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    assert torch.equal(m._prep[key][0], exp)
+    assert not torch.equal(before, exp)

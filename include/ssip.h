@@ -78,6 +78,17 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
 /* dx = conv_transpose(dy, w) (+ dx_add, nullable); w_crsk: [C][R][S][K] */
 int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, void* dx,
                     const void* dx_add, void* stream);
+/* DGRAD with the next-lower BatchNorm's backward reduction fused into the
+ * epilogue (replaces ssip_conv_dgrad + the reduce pass of ssip_bn_bwd):
+ *   dpre = (dgrad(dy) + dx_add) * (zmask > 0)          [N][H][W][C]
+ *   partial[tile][c] = { sum dpre, sum dpre * (y - mean[c]) * invstd[c] }
+ * zmask / y / mean / invstd belong to the BN+ReLU that produced this conv's
+ * input; dx_add (nullable) may alias dpre. */
+int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d);
+int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype);
+int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
+                       const void* zmask, const void* y, const float* mean, const float* invstd, void* dpre,
+                       float* partial, void* stream);
 int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d);
 /* dw_kcrs (fp32, torchvision layout [K][c_real][R][s_real]) (+)= dW */
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
@@ -101,6 +112,12 @@ int64_t ssip_bn_bwd_partial_floats(int64_t M, int C);
 int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
                 const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
                 void* dpre, float* partial, float* coef, void* stream);
+/* Finish a BN backward whose reduction came from ssip_conv_dgrad_bn's partials
+ * ([tiles][C][2] sums of dout and dout*xhat; dout already ReLU-masked):
+ * dgamma/dbeta (+)= ..., dy = dBN(dout). */
+int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const float* partial, const void* dout,
+                              const void* y, const float* mean, const float* invstd, const float* gamma,
+                              float* dgamma, float* dbeta, int accumulate, void* dy, float* coef, void* stream);
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream);
 
 /* ------------------------------------------------------------------------
@@ -142,14 +159,17 @@ typedef struct ssip_aug_param {
 int ssip_resize_h_u8(int B, const uint8_t* src, int64_t src_batch_stride, int Hs, int Ws, int Wo, int ksize,
                      const int* bounds, const int* coeffs, uint8_t* tmp, void* stream);
 /* vertical pass (ksize_v > 0) or none, then flip/rotate/photometric/cutout in the Hr x Wr frame,
- * crop (crop_x, crop_y, Wo, Ho), ToTensor + Normalize -> out [B][Ho][Wo][4] (channel 3 = 0).
+ * crop (crop_x, crop_y, Wo, Ho), ToTensor + Normalize -> out [B][Ho+2p][Wo+2p][4] (channel 3 = 0,
+ * a zero border of p = out_pad pixels: the stem conv's padding, pre-applied so the stem reads
+ * aligned pixel pairs with no bounds checks).
  * mean3/std3 are HOST pointers; params (nullable) is a device array of B entries. */
 int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stride, int src_h, int src_w, int Hr,
                     int Wr, int Ho, int Wo, int crop_x, int crop_y, int ksize_v, const int* bounds_v,
                     const int* coeffs_v, const ssip_aug_param* params, const float* mean3, const float* std3,
-                    void* out, void* stream);
-/* f32 NCHW (the nn.Module input contract) -> NHWC with Cp >= C channels */
-int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, const float* x, void* out, void* stream);
+                    int out_pad, void* out, void* stream);
+/* f32 NCHW (the nn.Module input contract) -> NHWC with Cp >= C channels and an out_pad zero border */
+int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, int out_pad, const float* x, void* out,
+                      void* stream);
 
 /* ------------------------------------------------------------------------
  * Optimizer and weight preparation

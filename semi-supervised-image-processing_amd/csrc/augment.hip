@@ -22,6 +22,11 @@
 
 namespace {
 
+template <typename T>
+struct __attribute__((aligned(4 * sizeof(T)))) Vec4Px {
+  T v[4];
+};
+
 // tmp[b][row][xo][ch] = clip8(sum_t src[b][row][xmin+t][ch] * k[xo][t] >> 22)
 __global__ void resize_h_kernel(int B, const uint8_t* __restrict__ src, long src_bstride, int Hs, int Ws, int Wo,
                                 int ksize, const int* __restrict__ bounds, const int* __restrict__ coeffs,
@@ -54,13 +59,21 @@ __global__ void augment_kernel(int B, const uint8_t* __restrict__ src, long src_
                                int Hr, int Wr, int Ho, int Wo, int cx, int cy, int ksize_v,
                                const int* __restrict__ bounds_v, const int* __restrict__ coeffs_v,
                                const ssip_aug_param* __restrict__ params, float m0, float m1, float m2, float s0,
-                               float s1, float s2, T* __restrict__ out) {
-  const long total = (long)B * Ho * Wo;
+                               float s1, float s2, int opad, T* __restrict__ out) {
+  const int Hp = Ho + 2 * opad, Wp = Wo + 2 * opad;
+  const long total = (long)B * Hp * Wp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int x = (int)(i % Wo);
-    const long t = i / Wo;
-    const int y = (int)(t % Ho);
-    const int b = (int)(t / Ho);
+    const int x = (int)(i % Wp) - opad;
+    const long t = i / Wp;
+    const int y = (int)(t % Hp) - opad;
+    const int b = (int)(t / Hp);
+    if (x < 0 || x >= Wo || y < 0 || y >= Ho) {  // zero border of a pre-padded stem input
+      Vec4Px<T> z;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) z.v[c] = from_f32<T>(0.f);
+      *reinterpret_cast<Vec4Px<T>*>(out + i * 4) = z;
+      continue;
+    }
     const ssip_aug_param pa = params ? params[b] : ssip_aug_param{};
     const int xr = x + cx, yr = y + cy;
     int xin = xr, yin = yr;
@@ -107,28 +120,31 @@ __global__ void augment_kernel(int B, const uint8_t* __restrict__ src, long src_
       }
     }
     if (xr >= pa.cut_x0 && xr < pa.cut_x1 && yr >= pa.cut_y0 && yr < pa.cut_y1) v[0] = v[1] = v[2] = 0.5f;
-    T* o = out + i * 4;
-    o[0] = from_f32<T>((v[0] - m0) / s0);
-    o[1] = from_f32<T>((v[1] - m1) / s1);
-    o[2] = from_f32<T>((v[2] - m2) / s2);
-    o[3] = from_f32<T>(0.f);
+    Vec4Px<T> o;
+    o.v[0] = from_f32<T>((v[0] - m0) / s0);
+    o.v[1] = from_f32<T>((v[1] - m1) / s1);
+    o.v[2] = from_f32<T>((v[2] - m2) / s2);
+    o.v[3] = from_f32<T>(0.f);
+    *reinterpret_cast<Vec4Px<T>*>(out + i * 4) = o;
   }
   (void)src_h;
 }
 
 // f32 NCHW -> T NHWC with channel padding (zeros)
 template <typename T>
-__global__ void nchw_to_nhwc_kernel(int B, int C, int H, int W, int Cp, const float* __restrict__ x,
+__global__ void nchw_to_nhwc_kernel(int B, int C, int H, int W, int Cp, int opad, const float* __restrict__ x,
                                     T* __restrict__ out) {
-  const long total = (long)B * H * W * Cp;
+  const int Hp = H + 2 * opad, Wp = W + 2 * opad;
+  const long total = (long)B * Hp * Wp * Cp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % Cp);
     const long t = i / Cp;
-    const int w = (int)(t % W);
-    const long t2 = t / W;
-    const int h = (int)(t2 % H);
-    const int b = (int)(t2 / H);
-    const float v = c < C ? x[(((long)b * C + c) * H + h) * W + w] : 0.f;
+    const int w = (int)(t % Wp) - opad;
+    const long t2 = t / Wp;
+    const int h = (int)(t2 % Hp) - opad;
+    const int b = (int)(t2 / Hp);
+    const bool in = c < C && h >= 0 && h < H && w >= 0 && w < W;
+    const float v = in ? x[(((long)b * C + c) * H + h) * W + w] : 0.f;
     out[i] = from_f32<T>(v);
   }
 }
@@ -157,29 +173,31 @@ int ssip_resize_h_u8(int B, const uint8_t* src, int64_t src_batch_stride, int Hs
 int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stride, int src_h, int src_w, int Hr,
                     int Wr, int Ho, int Wo, int crop_x, int crop_y, int ksize_v, const int* bounds_v,
                     const int* coeffs_v, const ssip_aug_param* params, const float* mean3, const float* std3,
-                    void* out, void* stream) {
+                    int out_pad, void* out, void* stream) {
   SSIP_REQUIRE(B > 0 && src && Hr > 0 && Wr > 0 && Ho > 0 && Wo > 0 && mean3 && std3 && out, SSIP_ERR_ARG,
                "ssip_augment_u8: bad arguments");
   SSIP_REQUIRE(crop_x >= 0 && crop_y >= 0 && crop_x + Wo <= Wr && crop_y + Ho <= Hr, SSIP_ERR_ARG,
                "ssip_augment_u8: crop window outside the resized image");
   SSIP_REQUIRE(src_w == Wr && (ksize_v > 0 ? (bounds_v && coeffs_v) : src_h == Hr), SSIP_ERR_ARG,
                "ssip_augment_u8: source geometry does not match the resize plan");
-  const long total = (long)B * Ho * Wo;
+  SSIP_REQUIRE(out_pad >= 0 && out_pad <= 8, SSIP_ERR_ARG, "ssip_augment_u8: out_pad must be 0..8");
+  const long total = (long)B * (Ho + 2 * out_pad) * (Wo + 2 * out_pad);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(augment_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, src,
                        (long)src_batch_stride, src_h, src_w, Hr, Wr, Ho, Wo, crop_x, crop_y, ksize_v, bounds_v,
-                       coeffs_v, params, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], (T*)out);
+                       coeffs_v, params, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], out_pad, (T*)out);
   });
   return ::ssip::check_launch("augment_u8");
 }
 
-int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, const float* x, void* out, void* stream) {
-  SSIP_REQUIRE(B > 0 && C > 0 && Cp >= C && H > 0 && W > 0 && x && out, SSIP_ERR_ARG,
-               "ssip_nchw_to_nhwc: bad arguments");
-  const long total = (long)B * H * W * Cp;
+int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, int out_pad, const float* x, void* out,
+                      void* stream) {
+  SSIP_REQUIRE(B > 0 && C > 0 && Cp >= C && H > 0 && W > 0 && out_pad >= 0 && out_pad <= 8 && x && out,
+               SSIP_ERR_ARG, "ssip_nchw_to_nhwc: bad arguments");
+  const long total = (long)B * (H + 2 * out_pad) * (W + 2 * out_pad) * Cp;
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, C, H, W,
-                       Cp, x, (T*)out);
+                       Cp, out_pad, x, (T*)out);
   });
   return ::ssip::check_launch("nchw_to_nhwc");
 }

@@ -341,6 +341,24 @@ int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, 
   return ::ssip::check_launch("bn_bwd");
 }
 
+int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const float* partial, const void* dout,
+                              const void* y, const float* mean, const float* invstd, const float* gamma,
+                              float* dgamma, float* dbeta, int accumulate, void* dy, float* coef, void* stream) {
+  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && tiles > 0 && partial && dout && y && mean && invstd && dy && coef,
+               SSIP_ERR_ARG, "ssip_bn_bwd_from_partials: bad arguments");
+  SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG,
+               "ssip_bn_bwd_from_partials: unsupported size");
+  hipStream_t st = (hipStream_t)stream;
+  const int total8 = (int)(M * C / 8);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, C, tiles, (long)M, partial, gamma, mean,
+                     invstd, dgamma, dbeta, accumulate, coef);
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
+                       (const T*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr);
+  });
+  return ::ssip::check_launch("bn_bwd_from_partials");
+}
+
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream) {
   SSIP_REQUIRE(n > 0 && n % 8 == 0 && g && z && out, SSIP_ERR_ARG, "ssip_relu_bwd: bad arguments");
   const long total8 = n / 8;

@@ -64,6 +64,13 @@ struct ConvArgs {
   void* out;
   const void* add;
   float* partial;
+  // DGRAD post-op (BN backward of the layer that produced this conv's input):
+  // out = (dgrad + add) * (pmask > 0); per-(tile, channel) sums of out and
+  // out * (py - pmean) * pinvstd into partial [tiles_m][Ng][2].
+  const void* pmask;
+  const void* py;
+  const float* pmean;
+  const float* pinvstd;
 };
 
 template <typename T> struct Traits;
@@ -197,9 +204,129 @@ struct Smem {
 // shared epilogue: WGRAD -> fp32 slab; FWD/DGRAD -> LDS-staged 16-B stores
 // (+ residual-gradient add for DGRAD, + BN partial statistics for FWD)
 // ---------------------------------------------------------------------------
+// DGRAD epilogue with the BatchNorm-backward reduction fused in (the tile is
+// already staged in LDS as T).  Each thread owns one 8-channel chunk (NT is a
+// multiple of BN/8), so its sums stay in registers; the NT/(BN/8) partial
+// sums per chunk are combined in fixed order through LDS.
+// The epilogue operands of the fused BN backward (mask z, pre-BN y and the
+// residual-gradient add) for the rows this thread stores; the LDS-DMA kernel
+// loads them before its main loop so the epilogue never waits on HBM.
+template <typename T, int BM, int BN, int NT>
+struct BnPostRegs {
+  static constexpr int CPR = BN / 8;
+  static constexpr int RPI = NT / CPR;  // rows per pass
+  static constexpr int ROWS = BM / RPI;
+  static_assert(NT % CPR == 0 && BM % RPI == 0, "thread count must cover whole rows");
+  Vec8<T> z[ROWS], y[ROWS], add[ROWS];
+
+  __device__ __forceinline__ void load(const ConvArgs& a, int m0, int n0) {
+    const int tid = threadIdx.x;
+    const int ch = tid % CPR, rsub = tid / CPR;
+    const int n = n0 + ch * 8;
+    if (n >= a.Ng) return;
+    const T* Zm = static_cast<const T*>(a.pmask);
+    const T* Yp = static_cast<const T*>(a.py);
+    const T* Add = static_cast<const T*>(a.add);
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int m = m0 + rsub + k * RPI;
+      if (m < a.M) {
+        const long off = (long)m * a.Ng + n;
+        z[k].load(Zm + off);
+        y[k].load(Yp + off);
+        if (Add) add[k].load(Add + off);
+      }
+    }
+  }
+};
+
+template <typename T, int BM, int BN, int NT>
+__device__ __forceinline__ void dgrad_bn_post(const ConvArgs& a, char* smem, int m0, int n0, int tm,
+                                              const BnPostRegs<T, BM, BN, NT>& pr) {
+  constexpr int CPR = BN / 8;
+  constexpr int RPI = NT / CPR;  // rows per pass
+  constexpr int ROWS = BM / RPI;
+  constexpr int EROW = BN * (int)sizeof(T) + 16;
+  const int tid = threadIdx.x;
+  const int ch = tid % CPR, rsub = tid / CPR;
+  const int n = n0 + ch * 8;
+  T* Out = static_cast<T*>(a.out);
+  const bool has_add = a.add != nullptr;
+  float sd[8], sx[8], mu[8], is[8];
+  const bool nok = n < a.Ng;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sd[j] = 0.f;
+    sx[j] = 0.f;
+    mu[j] = nok ? a.pmean[n + j] : 0.f;
+    is[j] = nok ? a.pinvstd[n + j] : 0.f;
+  }
+  if (nok) {
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int row = rsub + k * RPI;
+      const int m = m0 + row;
+      if (m >= a.M) break;
+      Vec8<T> v;
+      const char* src = smem + row * EROW + ch * 8 * (int)sizeof(T);
+      if constexpr (sizeof(T) == 2) {
+        v.v = *reinterpret_cast<const i32x4*>(src);
+      } else {
+        reinterpret_cast<Vec8<float>&>(v).v0 = reinterpret_cast<const i32x4*>(src)[0];
+        reinterpret_cast<Vec8<float>&>(v).v1 = reinterpret_cast<const i32x4*>(src)[1];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = v.get(j);
+        if (has_add) d += pr.add[k].get(j);
+        d = pr.z[k].get(j) > 0.f ? d : 0.f;
+        v.set(j, d);
+        const float dq = v.get(j);  // the stored (rounded) value feeds the sums
+        sd[j] += dq;
+        sx[j] += dq * ((pr.y[k].get(j) - mu[j]) * is[j]);
+      }
+      v.store(Out + (long)m * a.Ng + n);
+    }
+  }
+  // lanes l, l+CPR, ... of a wave share a chunk: butterfly over the lane
+  // bits above log2(CPR), then combine the waves in fixed order via LDS.
+  static_assert(CPR == 8 || CPR == 16, "chunk count per row");
+#pragma unroll
+  for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sd[j] += __shfl_xor(sd[j], o, 64);
+      sx[j] += __shfl_xor(sx[j], o, 64);
+    }
+  }
+  __syncthreads();
+  constexpr int NW = NT / 64;
+  float* red = reinterpret_cast<float*>(smem);  // [NW][CPR][16]
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane < CPR) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wave * CPR + lane) * 16 + j] = sd[j];
+      red[(wave * CPR + lane) * 16 + 8 + j] = sx[j];
+    }
+  }
+  __syncthreads();
+  if (tid < CPR * 16) {
+    const int c8 = tid >> 4, v = tid & 15;  // chunk, value (0-7 sum d, 8-15 sum d*xhat)
+    const int nn = n0 + c8 * 8;
+    if (nn < a.Ng) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += red[(w * CPR + c8) * 16 + v];
+      a.partial[((long)tm * a.Ng + nn + (v & 7)) * 2 + (v >> 3)] = t;
+    }
+  }
+}
+
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
-                                                   int n0, int tm) {
+                                                   int n0, int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
+                                                   bool pre_loaded) {
   constexpr int NT = 64 * WMW * WNW;
   constexpr int WTM = BM / WMW, WTN = BN / WNW;
   const int tid = threadIdx.x;
@@ -239,6 +366,18 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
         }
   }
   __syncthreads();
+  if constexpr (MODE == MODE_DGRAD) {
+    if (a.pmask != nullptr) {
+      if (pre_loaded) {
+        dgrad_bn_post<T, BM, BN, NT>(a, smem, m0, n0, tm, pre);
+      } else {
+        BnPostRegs<T, BM, BN, NT> pr;
+        pr.load(a, m0, n0);
+        dgrad_bn_post<T, BM, BN, NT>(a, smem, m0, n0, tm, pr);
+      }
+      return;
+    }
+  }
   {
     // each thread moves 8-element chunks: BN/8 chunks per row
     constexpr int CPR = BN / 8;
@@ -345,7 +484,14 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
                                               int tm) {
-  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm);
+  BnPostRegs<T, BM, BN, 64 * WMW * WNW> none;
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false);
+}
+
+template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
+                                              int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre) {
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, pre, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -635,8 +781,21 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE>
-__global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArgs a) {
+// Waves per SIMD the LDS budget allows; asking the compiler for that many
+// keeps the register count from costing a resident workgroup.
+constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
+  const int stage = wg ? 64 * (bm + bn) * 2 : (bm + bn) * 128;
+  const int blocks = 163840 / (nstage * stage);
+  const int w = blocks * nw / 4;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+// C4: the stem conv on a pre-padded 4-channel image (pad 0, S padded to 8,
+// even W): a 16-B chunk is a pixel pair (s, s+1) of one filter row, so a
+// 64-deep k-step covers filter rows 2ks and 2ks+1; k >= R*S*4 reads zeros.
+template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false>
+__global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
+    conv_glds_kernel(const ConvArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, BK = 64;
   constexpr int WTM = BM / WMW, WTN = BN / WNW;
@@ -710,6 +869,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArg
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       const int n = n0 + row;
       b_ok[t] = n < a.Ng;
+      b_c[t] = c;
       b_ptr[t] = Bg + (long)(b_ok[t] ? n : 0) * a.Kg + c * 8;
     }
   } else {
@@ -744,7 +904,17 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArg
   auto issue = [&](int ks, int stage) {
     char* As = smem + stage * STAGE;
     char* Bs = As + A_BYTES;
-    if constexpr (MODE == MODE_FWD) {
+    if constexpr (MODE == MODE_FWD && C4) {
+#pragma unroll
+      for (int t = 0; t < LA; ++t) {
+        const int k = ks * BK + a_c[t] * 8;
+        const int hin = a_h[t] + 2 * ks + (a_c[t] >> 2), win = a_w[t] + 2 * (a_c[t] & 3);
+        const bool ok = a_ok[t] && k < a.Kg && hin >= 0 && hin < a.H && win >= 0 && win + 1 < a.W;
+        const T* src = ok ? Ag + ((long)(a_base[t] + hin * a.W + win)) * 4
+                          : reinterpret_cast<const T*>(g_zero16);
+        glds16(src, As + (wave + NW * t) * 1024);
+      }
+    } else if constexpr (MODE == MODE_FWD) {
 #pragma unroll
       for (int t = 0; t < LA; ++t) {
         const int hin = a_h[t] + kr, win = a_w[t] + ks_;
@@ -773,7 +943,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArg
     if constexpr (!WG) {
 #pragma unroll
       for (int t = 0; t < LB; ++t) {
-        const T* src = b_ok[t] ? b_ptr[t] + ks * BK : reinterpret_cast<const T*>(g_zero16);
+        bool ok = b_ok[t];
+        if constexpr (C4) ok = ok && ks * BK + b_c[t] * 8 < a.Kg;
+        const T* src = ok ? b_ptr[t] + ks * BK : reinterpret_cast<const T*>(g_zero16);
         glds16(src, Bs + (wave + NW * t) * 1024);
       }
     } else {
@@ -825,6 +997,11 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArg
   // with a counted vmcnt (the later in-flight steps stay outstanding across
   // the raw barrier), then refill the slot every wave finished reading in
   // step ks-1.
+  // fused-BN epilogue operands: issued first, landed long before the epilogue
+  BnPostRegs<T, BM, BN, 64 * WMW * WNW> post;
+  if constexpr (MODE == MODE_DGRAD) {
+    if (a.pmask != nullptr) post.load(a, m0, n0);
+  }
   if (nsteps > 0) issue(0, 0);
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
@@ -855,7 +1032,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_glds_kernel(const ConvArg
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();
-  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm);
+  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -904,6 +1081,7 @@ struct Plan {
   int bm, bn, wmw, wnw;
   int stages;  // 2/3: LDS-DMA ring kernel (bf16); 0: register-staged kernel
   bool conv1;
+  bool stem_glds;  // conv1 on a pre-padded image (pad 0, even W): LDS-DMA capable
   ConvArgs args;
   dim3 grid;
   int splits;
@@ -935,7 +1113,7 @@ static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
   }
 }
 
-static bool glds_has(int mode, int bm, int bn, int wm, int wn, int st);
+static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st);
 
 // Default LDS-DMA configuration for a bf16 GEMM view (M x Ng, reduction Kg).
 // Chosen from tools/tune_conv.py over the ResNet-18 train-step shapes
@@ -959,12 +1137,12 @@ static int apply_force(int mode, int elem_bytes, Plan& pl) {
   const char* e = getenv("SSIP_CONV_FORCE");
   if (!e || !e[0]) return SSIP_OK;
   const char want = mode == MODE_FWD ? 'f' : mode == MODE_DGRAD ? 'd' : 'w';
-  if (e[0] != want || pl.conv1) return SSIP_OK;
+  if (e[0] != want || (pl.conv1 && !pl.stem_glds)) return SSIP_OK;
   int bm, bn, wm, wn, st;
   SSIP_REQUIRE(sscanf(e + 1, ",%d,%d,%d,%d,%d", &bm, &bn, &wm, &wn, &st) == 5, SSIP_ERR_ARG,
                "bad SSIP_CONV_FORCE '%s'", e);
   if (st > 0) {
-    SSIP_REQUIRE(elem_bytes == 2 && glds_has(mode, bm, bn, wm, wn, st), SSIP_ERR_ARG,
+    SSIP_REQUIRE(elem_bytes == 2 && glds_has(mode, pl.conv1, bm, bn, wm, wn, st), SSIP_ERR_ARG,
                  "SSIP_CONV_FORCE: no LDS-DMA kernel %s", e);
   } else {
     const bool ok = mode == MODE_WGRAD ? (wm == 2 && wn == 2 && (bm == 128 || bm == 64))
@@ -1014,7 +1192,8 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
     if (a.Ng % 128 != 0 && a.Ng % 64 == 0 && pl.bm == 128) pl.bn = 64;
   }
   pl.stages = 0;
-  if (elem_bytes == 2 && !pl.conv1) choose_glds(mode, a, pl);
+  pl.stem_glds = pl.conv1 && d->pad == 0 && d->W % 2 == 0 && d->S == 8;
+  if (elem_bytes == 2 && (!pl.conv1 || pl.stem_glds)) choose_glds(mode, a, pl);
   if (int rc = apply_force(mode, elem_bytes, pl)) return rc;
   if (mode == MODE_WGRAD) {
     const int tiles = ceil_div(a.M, pl.bm) * ceil_div(a.Ng, pl.bn);
@@ -1050,11 +1229,15 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
   X(64, 128, 1, 8, 2)
 
-static bool glds_has(int mode, int bm, int bn, int wm, int wn, int st) {
+#define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
+
+static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st) {
 #define SSIP_GLDS_EQ(BM_, BN_, WM_, WN_, ST_) \
   if (bm == BM_ && bn == BN_ && wm == WM_ && wn == WN_ && st == ST_) return true;
   if (mode == MODE_WGRAD) {
     SSIP_GLDS_WG(SSIP_GLDS_EQ)
+  } else if (mode == MODE_FWD && stem) {
+    SSIP_GLDS_STEM(SSIP_GLDS_EQ)
   } else {
     SSIP_GLDS_FD(SSIP_GLDS_EQ)
   }
@@ -1073,6 +1256,20 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
   if constexpr (MODE == MODE_WGRAD) {
     SSIP_GLDS_WG(SSIP_GLDS_GO)
   } else {
+    if constexpr (MODE == MODE_FWD) {
+      if (pl.conv1) {
+#define SSIP_GLDS_GO4(BM_, BN_, WM_, WN_, ST_)                                                                \
+  if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, true>), pl.grid, dim3(64 * WM_ * WN_), \
+                       0, st, pl.args);                                                                       \
+    return ::ssip::check_launch("conv_glds_stem");                                                            \
+  }
+        SSIP_GLDS_STEM(SSIP_GLDS_GO4)
+#undef SSIP_GLDS_GO4
+        ::ssip::set_error("no LDS-DMA stem kernel for %dx%d/%dx%d/%d", pl.bm, pl.bn, pl.wmw, pl.wnw, pl.stages);
+        return SSIP_ERR_ARG;
+      }
+    }
     SSIP_GLDS_FD(SSIP_GLDS_GO)
   }
 #undef SSIP_GLDS_GO
@@ -1169,6 +1366,34 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   if (rc) return rc;
   SSIP_REQUIRE(dy && w_crsk && dx, SSIP_ERR_ARG, "ssip_conv_dgrad: null pointer");
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
+  SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));
+}
+
+int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d) {
+  Plan pl;
+  if (plan_conv(MODE_DGRAD, d, 4, pl) != SSIP_OK) {
+    if (plan_conv(MODE_DGRAD, d, 2, pl) != SSIP_OK) return -1;
+  }
+  return (int64_t)ceil_div(pl.args.M, 128) * d->C * 2;
+}
+
+int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype) {
+  Plan pl;
+  if (plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
+  return ceil_div(pl.args.M, pl.bm);
+}
+
+int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
+                       const void* zmask, const void* y, const float* mean, const float* invstd, void* dpre,
+                       float* partial, void* stream) {
+  Plan pl;
+  int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
+  if (rc) return rc;
+  SSIP_REQUIRE(dy && w_crsk && zmask && y && mean && invstd && dpre && partial, SSIP_ERR_ARG,
+               "ssip_conv_dgrad_bn: null pointer");
+  SSIP_REQUIRE(pl.bm >= 128, SSIP_ERR_ARG, "ssip_conv_dgrad_bn: partial sizing assumes >= 128-row tiles");
+  pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dpre; pl.args.add = dx_add;
+  pl.args.pmask = zmask; pl.args.py = y; pl.args.pmean = mean; pl.args.pinvstd = invstd; pl.args.partial = partial;
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));
 }
 

@@ -66,6 +66,9 @@ _SIGS = {
     "ssip_conv_fwd_partial_tiles": (_c_int, [_PD, _c_int]),
     "ssip_conv_fwd": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_conv_dgrad_bn_partial_floats": (_c_i64, [_PD]),
+    "ssip_conv_dgrad_bn_partial_tiles": (_c_int, [_PD, _c_int]),
+    "ssip_conv_dgrad_bn": (_c_int, [_PD, _c_int] + [_vp] * 10),
     "ssip_conv_wgrad_workspace_bytes": (_c_i64, [_PD]),
     "ssip_conv_wgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _vp]),
     "ssip_bn_finalize": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
@@ -73,6 +76,7 @@ _SIGS = {
     "ssip_bn_apply": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "ssip_bn_bwd_partial_floats": (_c_i64, [_c_i64, _c_int]),
     "ssip_bn_bwd": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_bn_bwd_from_partials": (_c_int, [_c_int, _c_i64, _c_int, _c_int] + [_vp] * 8 + [_c_int, _vp, _vp, _vp]),
     "ssip_relu_bwd": (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp]),
     "ssip_maxpool_fwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),
     "ssip_maxpool_bwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),
@@ -84,9 +88,9 @@ _SIGS = {
     "ssip_resize_h_u8": (_c_int, [_c_int, _vp, _c_i64, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp]),
     "ssip_augment_u8": (
         _c_int,
-        [_c_int, _c_int, _vp, _c_i64] + [_c_int] * 9 + [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
+        [_c_int, _c_int, _vp, _c_i64] + [_c_int] * 9 + [_vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
     ),
-    "ssip_nchw_to_nhwc": (_c_int, [_c_int] * 6 + [_vp, _vp, _vp]),
+    "ssip_nchw_to_nhwc": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp]),
     "ssip_adamw": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_f, _vp]),
     "ssip_weight_prep": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp, _vp]),
     "ssip_weight_prep_batch": (_c_int, [_c_int, _c_int, ctypes.POINTER(WPrep), _vp]),
@@ -121,9 +125,13 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed ({rc}): {msg}")
 
 
+# int-returning queries (not status codes)
+_NOT_STATUS = ("ssip_version", "ssip_conv_fwd_partial_tiles", "ssip_conv_dgrad_bn_partial_tiles")
+
+
 def call(name: str, *args) -> int:
     fn = getattr(lib(), name)
     rc = fn(*args)
-    if _SIGS[name][0] is _c_int and name not in ("ssip_version", "ssip_conv_fwd_partial_tiles"):
+    if _SIGS[name][0] is _c_int and name not in _NOT_STATUS:
         check(rc, name)
     return rc

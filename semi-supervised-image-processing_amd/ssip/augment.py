@@ -184,8 +184,9 @@ class GpuTransform:
     """
 
     def __init__(self, size: int = 224, dtype: torch.dtype = torch.float32, mode: str = "resize",
-                 resize: int = 256, crop: int = 224, mean=IMAGENET_MEAN, std=IMAGENET_STD):
-        self.size, self.dtype, self.mode = size, dtype, mode
+                 resize: int = 256, crop: int = 224, mean=IMAGENET_MEAN, std=IMAGENET_STD, pad: int = 3):
+        # pad: zero border written around each image (the stem conv's padding, pre-applied)
+        self.size, self.dtype, self.mode, self.pad = size, dtype, mode, pad
         self.resize, self.crop = resize, crop
         import ctypes
 
@@ -238,10 +239,12 @@ class GpuTransform:
         kv, bv, cv = 0, None, None
         if Hr != H:
             bv, cv, kv = self._table(H, Hr, dev)
+        p = self.pad
+        shape = (B, Ho + 2 * p, Wo + 2 * p, 4)
         if out is None:
-            out = torch.empty((B, Ho, Wo, 4), device=dev, dtype=self.dtype)
-        elif out.shape != (B, Ho, Wo, 4) or out.dtype != self.dtype or not out.is_contiguous():
-            raise ValueError("GpuTransform: bad `out` buffer")
+            out = torch.empty(shape, device=dev, dtype=self.dtype)
+        elif tuple(out.shape) != shape or out.dtype != self.dtype or not out.is_contiguous():
+            raise ValueError(f"GpuTransform: `out` must be a contiguous {shape} {self.dtype} buffer")
         pptr = None
         if params is not None:
             params = params.to(dev, torch.int32).contiguous()
@@ -249,8 +252,8 @@ class GpuTransform:
             pptr = params.data_ptr()
         _lib.call("ssip_augment_u8", _lib.F32 if self.dtype == torch.float32 else _lib.BF16, B, src.data_ptr(),
                   bstride, src_h, src_w, Hr, Wr, Ho, Wo, cx, cy, kv, None if bv is None else bv.data_ptr(),
-                  None if cv is None else cv.data_ptr(), pptr, self.mean, self.std, out.data_ptr(), stream)
-        return DeviceImages(out)
+                  None if cv is None else cv.data_ptr(), pptr, self.mean, self.std, p, out.data_ptr(), stream)
+        return DeviceImages(out, p)
 
 
 def to_nchw(images: DeviceImages) -> torch.Tensor:

@@ -137,9 +137,14 @@ class HostImageBatch:
         params = self.params.to(dev, non_blocking=non_blocking)
         if isinstance(self.pixels, torch.Tensor):
             return tf(self.pixels.to(dev, non_blocking=non_blocking), params)
-        outs = [tf(p.unsqueeze(0).to(dev, non_blocking=non_blocking), params[i:i + 1]).nhwc4
-                for i, p in enumerate(self.pixels)]
-        return DeviceImages(torch.cat(outs, 0))
+        # ragged sources (eval/extraction): one launch per image into one padded batch buffer
+        out = None
+        for i, p in enumerate(self.pixels):
+            if out is None:
+                Hr, Wr, Ho, Wo, _, _ = tf.geometry(p.shape[0], p.shape[1])
+                out = torch.empty((len(self.pixels), Ho + 2 * tf.pad, Wo + 2 * tf.pad, 4), device=dev, dtype=dt)
+            tf(p.unsqueeze(0).to(dev, non_blocking=non_blocking), params[i:i + 1], out=out[i:i + 1])
+        return DeviceImages(out, tf.pad)
 
 
 _TF_CACHE = {}

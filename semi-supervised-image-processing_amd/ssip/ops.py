@@ -150,6 +150,38 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx: torch.Te
     call(*args)
 
 
+def conv_dgrad_bn_partial_floats(g: ConvGeom) -> int:
+    return int(_lib.lib().ssip_conv_dgrad_bn_partial_floats(g.desc()))
+
+
+def conv_dgrad_bn_partial_tiles(g: ConvGeom, dtype: torch.dtype) -> int:
+    t = int(_lib.lib().ssip_conv_dgrad_bn_partial_tiles(g.desc(), _DT[dtype]))
+    if t <= 0:
+        raise RuntimeError(_lib.lib().ssip_last_error().decode())
+    return t
+
+
+def conv_dgrad_bn(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx_add: Optional[torch.Tensor],
+                  zmask: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, invstd: torch.Tensor,
+                  dpre: torch.Tensor, partial: torch.Tensor) -> None:
+    """dpre = (dgrad(dy) + dx_add) * (zmask > 0) plus the BN-backward partial
+    sums of the BN that produced zmask (see include/ssip.h)."""
+    assert dy.numel() == g.N * g.P * g.Q * g.K, "conv_dgrad_bn: dy shape"
+    assert w_crsk.numel() == g.K * g.R * g.S * g.C, "conv_dgrad_bn: w shape"
+    n = g.N * g.H * g.W * g.C
+    assert dpre.numel() == n and zmask.numel() == n and y.numel() == n, "conv_dgrad_bn: activation shapes"
+    assert mean.numel() >= g.C and invstd.numel() >= g.C and mean.dtype == invstd.dtype == torch.float32
+    assert partial.dtype == torch.float32 and partial.numel() >= conv_dgrad_bn_partial_floats(g)
+    if dx_add is not None:
+        assert dx_add.numel() == n and dx_add.dtype == dpre.dtype
+    args = ("ssip_conv_dgrad_bn", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx_add), _p(zmask), _p(y),
+            _p(mean), _p(invstd), _p(dpre), _p(partial), stream_ptr())
+    if _timer is not None:
+        _timer.wrap("dgrad", g.flops(), call, *args)
+        return
+    call(*args)
+
+
 def conv_wgrad_workspace_bytes(g: ConvGeom) -> int:
     return int(_lib.lib().ssip_conv_wgrad_workspace_bytes(g.desc()))
 
@@ -216,6 +248,12 @@ def bn_bwd(M: int, C: int, dz, zmask, y, mean, invstd, gamma, dgamma, dbeta, acc
            coef) -> None:
     call("ssip_bn_bwd", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(y), _p(mean), _p(invstd), _p(gamma),
          _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(dpre), _p(partial), _p(coef), stream_ptr())
+
+
+def bn_bwd_from_partials(M: int, C: int, tiles: int, partial, dout, y, mean, invstd, gamma, dgamma, dbeta,
+                         accumulate: bool, dy, coef) -> None:
+    call("ssip_bn_bwd_from_partials", dtype_code(dout), M, C, tiles, _p(partial), _p(dout), _p(y), _p(mean),
+         _p(invstd), _p(gamma), _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(coef), stream_ptr())
 
 
 def relu_bwd(g, z, out) -> None:
@@ -291,9 +329,10 @@ def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
          float(beta2), float(eps), float(weight_decay), int(step), float(grad_scale), stream_ptr())
 
 
-def nchw_to_nhwc(x: torch.Tensor, Cp: int, dtype: torch.dtype) -> torch.Tensor:
+def nchw_to_nhwc(x: torch.Tensor, Cp: int, dtype: torch.dtype, pad: int = 0) -> torch.Tensor:
+    """f32 NCHW -> [B, H+2*pad, W+2*pad, Cp] with a zero border and zero channel padding."""
     B, C, H, W = x.shape
     x = x.contiguous().float()
-    out = torch.empty((B, H, W, Cp), device=x.device, dtype=dtype)
-    call("ssip_nchw_to_nhwc", _DT[dtype], B, C, H, W, Cp, _p(x), _p(out), stream_ptr())
+    out = torch.empty((B, H + 2 * pad, W + 2 * pad, Cp), device=x.device, dtype=dtype)
+    call("ssip_nchw_to_nhwc", _DT[dtype], B, C, H, W, Cp, pad, _p(x), _p(out), stream_ptr())
     return out

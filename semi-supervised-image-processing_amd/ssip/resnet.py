@@ -24,6 +24,8 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -100,15 +102,34 @@ _DTYPES = {"fp32": torch.float32, "f32": torch.float32, "float32": torch.float32
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
 
 
+STEM_PAD = 3  # torchvision conv1 padding; the input producers pre-apply it
+# dgrad epilogue + BN-backward reduction fusion (ssip_conv_dgrad_bn); see _backward
+_FUSE_BN_BWD = os.environ.get("SSIP_FUSE_BN_BWD") == "1"
+
+
 @dataclass
 class DeviceImages:
     """A batch already in the stem's NHWC4 layout and the engine dtype
-    (produced by ``ssip.augment``): skips the NCHW->NHWC conversion."""
+    (produced by ``ssip.augment``): skips the NCHW->NHWC conversion.
 
-    nhwc4: torch.Tensor
+    ``buf`` is [B, H+2*pad, W+2*pad, 4] with a zero border of ``pad`` pixels:
+    with pad == 3 (the stem conv's own padding) the stem runs as a pad-0 conv
+    whose 16-byte pixel-pair loads are aligned and never straddle the border.
+    """
+
+    buf: torch.Tensor
+    pad: int = 0
+
+    @property
+    def nhwc4(self) -> torch.Tensor:
+        """The unpadded [B, H, W, 4] image (a view)."""
+        p = self.pad
+        if p == 0:
+            return self.buf
+        return self.buf[:, p:self.buf.shape[1] - p, p:self.buf.shape[2] - p, :]
 
     def __len__(self):
-        return self.nhwc4.shape[0]
+        return self.buf.shape[0]
 
 
 class _Identity(nn.Module):
@@ -223,9 +244,11 @@ class SSIPResNet(nn.Module):
     # ------------------------------------------------------------------
     def forward(self, x):
         if isinstance(x, DeviceImages):
-            images = x.nhwc4
-            if images.dtype != self.compute_dtype:
-                images = images.to(self.compute_dtype)
+            images, pad = x.buf, x.pad
+            if pad not in (0, self.conv1.padding[0]):
+                images, pad = x.nhwc4, 0
+            if images.dtype != self.compute_dtype or not images.is_contiguous():
+                images = images.to(self.compute_dtype).contiguous()
         else:
             dev = self.conv1.weight.device
             if dev.type != "cuda":
@@ -233,20 +256,21 @@ class SSIPResNet(nn.Module):
             x = x.to(dev, non_blocking=True)
             if x.dim() != 4 or x.shape[1] != 3:
                 raise ValueError(f"expected a [B,3,H,W] batch, got {tuple(x.shape)}")
-            images = ops.nchw_to_nhwc(x, 4, self.compute_dtype)
+            pad = self.conv1.padding[0]
+            images = ops.nchw_to_nhwc(x, 4, self.compute_dtype, pad=pad)
         params = [p for p in self.parameters()]
         if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
             # inference (eval, pseudo-labelling, weak view, extraction): no autograd node, nothing saved
-            sv = _forward(self, images, train=self.training, save=False)
+            sv = _forward(self, images, train=self.training, save=False, in_pad=pad)
             return sv.feat.view(sv.N, -1, 1, 1) if self.embedding_only else sv.logits
-        return _NetFn.apply(self, images, *params)
+        return _NetFn.apply(self, images, pad, *params)
 
 
 class _NetFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, model: SSIPResNet, images: torch.Tensor, *params):
+    def forward(ctx, model: SSIPResNet, images: torch.Tensor, in_pad: int, *params):
         train = model.training
-        saved = _forward(model, images, train=train, save=train)
+        saved = _forward(model, images, train=train, save=train, in_pad=in_pad)
         ctx.model = model
         ctx.saved = saved
         out = saved.feat.view(saved.N, -1, 1, 1) if model.embedding_only else saved.logits
@@ -262,17 +286,23 @@ class _NetFn(torch.autograd.Function):
             raise RuntimeError("ssip: backward requires a train-mode forward with trainable parameters")
         _backward(model, saved, dlogits.contiguous().float())
         ctx.saved = None
-        return (None, None) + (None,) * len(list(model.parameters()))
+        return (None, None, None) + (None,) * len(list(model.parameters()))
 
 
 # ---------------------------------------------------------------------------
 # forward engine
 # ---------------------------------------------------------------------------
-def _geom(conv: nn.Conv2d, N: int, H: int, W: int) -> ConvGeom:
+def _geom(conv: nn.Conv2d, N: int, H: int, W: int, in_pad: int = 0) -> ConvGeom:
+    """in_pad: the input already carries a zero border of the conv's own
+    padding (H, W include it) -> a pad-0 conv over the padded image."""
     K, C, R, S = conv.weight.shape
     stem = C == 3
+    pad = conv.padding[0]
+    if in_pad:
+        assert in_pad == pad, "pre-padded input must carry exactly the conv padding"
+        pad = 0
     return ConvGeom(N=N, H=H, W=W, C=4 if stem else C, K=K, R=R, S=8 if stem else S,
-                    stride=conv.stride[0], pad=conv.padding[0], c_real=C, s_real=S)
+                    stride=conv.stride[0], pad=pad, c_real=C, s_real=S)
 
 
 def _prepare_weights(model: SSIPResNet, need_t: bool) -> None:
@@ -311,8 +341,8 @@ def _prepped(model: SSIPResNet, conv: nn.Conv2d, g: ConvGeom, need_t: bool):
 
 
 def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool, save: bool,
-             update_running: bool) -> _ConvRec:
-    g = _geom(conv, N, H, W)
+             update_running: bool, in_pad: int = 0) -> _ConvRec:
+    g = _geom(conv, N, H, W, in_pad)
     dt = model.compute_dtype
     krsc = _prepped(model, conv, g, need_t=save)[0]
     y = torch.empty((N, g.P, g.Q, g.K), device=x.device, dtype=dt)
@@ -331,7 +361,7 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
     return _ConvRec(geom=g, conv=conv, bn=bn, x=x, y=y, stats=stats)
 
 
-def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool) -> _Saved:
+def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, in_pad: int = 0) -> _Saved:
     N, H, W, C4 = images.shape
     dt = model.compute_dtype
     upd = train and model.bn_update_running
@@ -339,7 +369,7 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool) -
     dev = images.device
     _prepare_weights(model, need_t=save)
     # stem: conv 7x7/2 -> BN -> ReLU -> maxpool 3x3/2
-    rec = _conv_bn(model, model.conv1, model.bn1, images, N, H, W, train, save, upd)
+    rec = _conv_bn(model, model.conv1, model.bn1, images, N, H, W, train, save, upd, in_pad)
     g = rec.geom
     z1 = torch.empty_like(rec.y)
     ops.bn_apply(N * g.P * g.Q, g.K, rec.y, rec.stats[2], rec.stats[3], None, True, z1)
@@ -471,9 +501,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     workspace = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
     coef_buf = torch.empty(3 * 2048, device=dev, dtype=torch.float32)
 
-    def bn_backward(rec: _ConvRec, dzin, zmask, dpre=None):
-        g = rec.geom
-        M = N * g.P * g.Q
+    def bn_grads(rec: _ConvRec):
         bn = rec.bn
         dgam = dbet = None
         acc = False
@@ -484,10 +512,28 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
             if dgam is not None and acc2 != acc:
                 raise RuntimeError("ssip: BN weight/bias grads must both be fresh or both accumulate")
             acc = acc2
+        return dgam, dbet, acc
+
+    def bn_backward(rec: _ConvRec, dzin, zmask, dpre=None):
+        """BN(+ReLU) backward with its own reduction pass."""
+        g = rec.geom
+        M = N * g.P * g.Q
+        dgam, dbet, acc = bn_grads(rec)
         dy = torch.empty_like(rec.y)
         partial = torch.empty(ops.bn_bwd_partial_floats(M, g.K), device=dev, dtype=torch.float32)
-        ops.bn_bwd(M, g.K, dzin, zmask, rec.y, rec.stats[0], rec.stats[1], bn.weight.detach(), dgam, dbet, acc,
+        ops.bn_bwd(M, g.K, dzin, zmask, rec.y, rec.stats[0], rec.stats[1], rec.bn.weight.detach(), dgam, dbet, acc,
                    dy, dpre, partial, coef_buf[: 3 * g.K])
+        return dy
+
+    def bn_backward_fused(rec: _ConvRec, dpre, partial, tiles):
+        """BN backward whose reduction came out of the dgrad epilogue that
+        produced dpre (already ReLU-masked)."""
+        g = rec.geom
+        M = N * g.P * g.Q
+        dgam, dbet, acc = bn_grads(rec)
+        dy = torch.empty_like(rec.y)
+        ops.bn_bwd_from_partials(M, g.K, tiles, partial, dpre, rec.y, rec.stats[0], rec.stats[1],
+                                 rec.bn.weight.detach(), dgam, dbet, acc, dy, coef_buf[: 3 * g.K])
         return dy
 
     def conv_wgrad(rec: _ConvRec, dy):
@@ -501,40 +547,66 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         crsk = _prepped_t(model, rec)[1]
         ops.conv_dgrad(rec.geom, dy, crsk, out, add)
 
+    def conv_dgrad_bn(rec: _ConvRec, dy, below: _ConvRec, out, add=None):
+        """dgrad of `rec` fused with the mask + BN reduction of `below` (the
+        BN+ReLU whose output z is rec's input).  Off by default: measured on
+        MI355X (tools/time_bnpost.py) the epilogue's extra z/y reads cost more
+        than the reduction pass they replace (l1: 272 vs 233 us)."""
+        if not _FUSE_BN_BWD:
+            conv_dgrad(rec, dy, out, add)
+            return None
+        crsk = _prepped_t(model, rec)[1]
+        partial = torch.empty(ops.conv_dgrad_bn_partial_floats(rec.geom), device=dev, dtype=torch.float32)
+        ops.conv_dgrad_bn(rec.geom, dy, crsk, add, below.z, below.y, below.stats[0], below.stats[1], out, partial)
+        return out, partial, ops.conv_dgrad_bn_partial_tiles(rec.geom, dt)
+
     nblocks = len(sv.blocks)
     blocks = list(model.blocks())
+    pending = None  # (dpre, partial, tiles) of the current block's last BN, from the block above
     for bi in range(nblocks - 1, -1, -1):
         recs, ds, xin = sv.blocks[bi]
         stage_idx = bi + 1
         need_dx = first_trainable is not None and first_trainable < stage_idx
+        below = sv.blocks[bi - 1][0][-1] if bi > 0 else None  # BN+ReLU producing this block's input
         last = recs[-1]
-        dpre = torch.empty_like(last.y)
-        dy = bn_backward(last, dz, last.z, dpre)
+        if pending is None:
+            dpre = torch.empty_like(last.y)
+            dy = bn_backward(last, dz, last.z, dpre)
+        else:
+            dpre, part, tiles = pending
+            dy = bn_backward_fused(last, dpre, part, tiles)
+        pending = None
         dy_ds = None
         if ds is not None:
             dy_ds = bn_backward(ds, dpre, None)
         # main path, last conv back to the first
         g_cur = dy
+        dxin = None
         for i in range(len(recs) - 1, -1, -1):
             r = recs[i]
             conv_wgrad(r, g_cur)
             if i > 0:
                 dzp = torch.empty_like(r.x)
-                conv_dgrad(r, g_cur, dzp)
-                g_cur = bn_backward(recs[i - 1], dzp, recs[i - 1].z)
-            else:
-                if need_dx:
-                    dxin = torch.empty_like(xin)
-                    if ds is None:
-                        conv_dgrad(r, g_cur, dxin, dpre)
-                    else:
-                        conv_dgrad(r, g_cur, dxin)
+                fused = conv_dgrad_bn(r, g_cur, recs[i - 1], dzp)
+                if fused is None:
+                    g_cur = bn_backward(recs[i - 1], dzp, recs[i - 1].z)
                 else:
-                    dxin = None
+                    g_cur = bn_backward_fused(recs[i - 1], *fused)
+            elif need_dx:
+                dxin = torch.empty_like(xin)
+                if ds is None and below is not None:
+                    pending = conv_dgrad_bn(r, g_cur, below, dxin, dpre)
+                elif ds is None:
+                    conv_dgrad(r, g_cur, dxin, dpre)
+                else:
+                    conv_dgrad(r, g_cur, dxin)
         if ds is not None:
             conv_wgrad(ds, dy_ds)
             if dxin is not None:
-                conv_dgrad(ds, dy_ds, dxin, dxin)
+                if below is not None:
+                    pending = conv_dgrad_bn(ds, dy_ds, below, dxin, dxin)
+                else:
+                    conv_dgrad(ds, dy_ds, dxin, dxin)
         if hook is not None:
             hook(list(blocks[bi].parameters()))
         dz = dxin

@@ -67,7 +67,8 @@ class SemiStep:
         pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
         # 1. views: [labelled weak ; unlabelled strong] in one buffer, weak unlabelled separately
         S = self.size
-        x_ls = torch.empty((Bl + Bu, S, S, 4), device=dev, dtype=m.compute_dtype)
+        P = self.tf.pad
+        x_ls = torch.empty((Bl + Bu, S + 2 * P, S + 2 * P, 4), device=dev, dtype=m.compute_dtype)
         self.tf(x_l, pl, out=x_ls[:Bl])
         self.tf(x_u, ps, out=x_ls[Bl:])
         xw = self.tf(x_u, pw)
@@ -81,7 +82,7 @@ class SemiStep:
         self.opt.zero_grad(set_to_none=True)
         if self.bucketer is not None:
             self.bucketer.reset()
-        logits = m(DeviceImages(x_ls))
+        logits = m(DeviceImages(x_ls, P))
         # 4. loss + dlogits in one launch
         out, dzl, dzs, pseudo, mask = ops.semi_loss(logits[:Bl].detach().contiguous(), y_l,
                                                     zw.contiguous(), logits[Bl:].detach().contiguous(),

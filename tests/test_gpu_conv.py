@@ -19,17 +19,27 @@ SHAPES = [
     (3, 64, 7, 7, 192, 3, 1, 1),
     (2, 3, 32, 32, 64, 7, 2, 3),   # stem (C padded to 4, S to 8)
     (1, 256, 7, 7, 512, 3, 1, 1),
+    # stem on a pre-padded image (pad-0 conv over H+6 x W+6; the engine's layout)
+    (2, 3, 32, 32, 64, 7, 2, 3, True),
+    (3, 3, 56, 40, 64, 7, 2, 3, True),
 ]
 
 
-def _geom(N, C, H, W, K, R, st, pd):
+def _unpack(shape):
+    N, C, H, W, K, R, st, pd, *rest = shape
+    return N, C, H, W, K, R, st, pd, bool(rest and rest[0])
+
+
+def _geom(N, C, H, W, K, R, st, pd, pre=False):
     stem = C == 3
+    if pre:  # the input carries the conv padding as a zero border
+        H, W, pd = H + 2 * pd, W + 2 * pd, 0
     return ConvGeom(N=N, H=H, W=W, C=4 if stem else C, K=K, R=R, S=8 if stem else R, stride=st, pad=pd,
                     c_real=C, s_real=R)
 
 
-def _to_nhwc(x, Cp, dt, dev):
-    return ops.nchw_to_nhwc(x.to(dev), Cp, dt)
+def _to_nhwc(x, Cp, dt, dev, pad=0):
+    return ops.nchw_to_nhwc(x.to(dev), Cp, dt, pad=pad)
 
 
 def _relerr(a, b):
@@ -40,16 +50,16 @@ def _relerr(a, b):
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])
 def test_conv_fwd(dev, shape, dtname):
     torch.manual_seed(0)
-    N, C, H, W, K, R, st, pd = shape
+    N, C, H, W, K, R, st, pd, pre = _unpack(shape)
     dt = torch.float32 if dtname == "f32" else torch.bfloat16
-    g = _geom(*shape)
+    g = _geom(*_unpack(shape))
     x = torch.randn(N, C, H, W)
     w = torch.randn(K, C, R, R) * 0.1
     if dt == torch.bfloat16:
         x = x.bfloat16().float()
         w = w.bfloat16().float()
     ref = F.conv2d(x.double(), w.double(), stride=st, padding=pd).permute(0, 2, 3, 1)
-    xh = _to_nhwc(x, g.C, dt, dev)
+    xh = _to_nhwc(x, g.C, dt, dev, pd if pre else 0)
     krsc = torch.empty((K, R, g.S, g.C), device=dev, dtype=dt)
     ops.weight_prep(w.to(dev), dt, g.C, g.S, krsc, None)
     y = torch.empty((N, g.P, g.Q, K), device=dev, dtype=dt)
@@ -77,7 +87,7 @@ def test_conv_fwd(dev, shape, dtname):
     assert _relerr(rv.cpu(), 0.9 + 0.1 * r.var(0, unbiased=True)) < tol_s * 10
 
 
-@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3])
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3 and len(s) == 8])
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])
 def test_conv_dgrad(dev, shape, dtname):
     torch.manual_seed(1)
@@ -106,15 +116,15 @@ def test_conv_dgrad(dev, shape, dtname):
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])
 def test_conv_wgrad(dev, shape, dtname):
     torch.manual_seed(2)
-    N, C, H, W, K, R, st, pd = shape
+    N, C, H, W, K, R, st, pd, pre = _unpack(shape)
     dt = torch.float32 if dtname == "f32" else torch.bfloat16
-    g = _geom(*shape)
+    g = _geom(*_unpack(shape))
     x = torch.randn(N, C, H, W)
     dy = torch.randn(N, K, g.P, g.Q)
     if dt == torch.bfloat16:
         x, dy = x.bfloat16().float(), dy.bfloat16().float()
     ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, R, R), dy.double(), stride=st, padding=pd)
-    xh = _to_nhwc(x, g.C, dt, dev)
+    xh = _to_nhwc(x, g.C, dt, dev, pd if pre else 0)
     dyh = _to_nhwc(dy, K, dt, dev)
     dw = torch.full((K, C, R, R), 7.0, device=dev)
     ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
@@ -126,3 +136,46 @@ def test_conv_wgrad(dev, shape, dtname):
     ops.conv_wgrad(g, dyh, xh, dw, True, ws)
     torch.cuda.synchronize()
     assert _relerr(dw.cpu(), 2 * ref) < tol
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3 and len(s) == 8])
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_conv_dgrad_bn_fused(dev, shape, dtname, with_add):
+    """dgrad epilogue fused with the ReLU mask and the BN-backward partial
+    sums of the layer below: dpre = (dgrad + add) * (z > 0),
+    sum(dpre), sum(dpre * (y - mean) * invstd) per channel."""
+    torch.manual_seed(3)
+    N, C, H, W, K, R, st, pd = shape
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    g = _geom(*shape)
+    w = torch.randn(K, C, R, R) * 0.1
+    dy = torch.randn(N, K, g.P, g.Q)
+    add = torch.randn(N, C, H, W)
+    y = torch.randn(N, C, H, W) * 2 + 0.5
+    z = torch.relu(torch.randn(N, C, H, W))
+    if dt == torch.bfloat16:
+        w, dy, add, y, z = (t.bfloat16().float() for t in (w, dy, add, y, z))
+    mean = torch.randn(C) * 0.1
+    invstd = torch.rand(C) + 0.5
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.double(), dy.double(), stride=st, padding=pd)
+    if with_add:
+        ref = ref + add.double()
+    ref = ref * (z > 0).double()
+    xhat = (y.double() - mean.double()[None, :, None, None]) * invstd.double()[None, :, None, None]
+    sum_d = ref.sum((0, 2, 3))
+    sum_dx = (ref * xhat).sum((0, 2, 3))
+    crsk = torch.empty((C, R, R, K), device=dev, dtype=dt)
+    ops.weight_prep(w.to(dev), dt, C, R, None, crsk)
+    dpre = torch.empty((N, H, W, C), device=dev, dtype=dt)
+    part = torch.full((ops.conv_dgrad_bn_partial_floats(g),), float("nan"), device=dev)
+    ops.conv_dgrad_bn(g, _to_nhwc(dy, K, dt, dev), crsk, _to_nhwc(add, C, dt, dev) if with_add else None,
+                      _to_nhwc(z, C, dt, dev), _to_nhwc(y, C, dt, dev), mean.to(dev), invstd.to(dev), dpre, part)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    assert _relerr(dpre.cpu(), ref.permute(0, 2, 3, 1)) < tol
+    tiles = ops.conv_dgrad_bn_partial_tiles(g, dt)
+    p = part[: tiles * C * 2].view(tiles, C, 2).double().sum(0).cpu()
+    tol_s = 1e-4 if dt == torch.float32 else 2e-2
+    assert _relerr(p[:, 0], sum_d) < tol_s
+    assert _relerr(p[:, 1], sum_dx) < tol_s

@@ -130,3 +130,27 @@ def test_frozen_backbone_only_fc_grads(dev):
             assert p.grad is None
     # running stats still updated in frozen-backbone train mode (reference quirk)
     assert _relerr(mine.bn1.running_mean, ref.bn1.running_mean) < 1e-3
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_bn_backward_path_matches(dev, dtype, monkeypatch):
+    """The dgrad-epilogue BN-backward fusion (ssip_conv_dgrad_bn +
+    ssip_bn_bwd_from_partials) gives the same gradients as the separate
+    reduction pass (only the summation order differs)."""
+    import ssip.resnet as R
+    torch.manual_seed(5)
+    x = torch.randn(4, 3, 64, 64)
+    y = torch.randint(0, 2, (4,))
+    grads = []
+    for fuse in (False, True):
+        monkeypatch.setattr(R, "_FUSE_BN_BWD", fuse)
+        _, mine = _pair(dtype=dtype)
+        mine = mine.to(dev).train()
+        out = mine(x.to(dev))
+        torch.nn.functional.cross_entropy(out.float(), y.to(dev)).backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()})
+    tol = 1e-4 if dtype == "fp32" else 5e-2
+    for k in grads[0]:
+        assert _cos(grads[0][k], grads[1][k]) > (0.99999 if dtype == "fp32" else 0.99), k
+        assert _relerr(grads[1][k], grads[0][k]) < tol, k

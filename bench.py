@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--labeled", type=int, default=128)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial-weak", action="store_true", help="run the weak forward on the main stream (A/B)")
     return ap.parse_args()
 
 
@@ -71,6 +72,7 @@ def main():
             dist.broadcast(b, 0)
     bucketer = GradBucketer(model.flatten_parameters()) if world > 1 else None
     step = SemiStep(model, lr=1e-4, weight_decay=1e-4, tau=0.7, bucketer=bucketer, seed=rank)
+    step.overlap = not args.serial_weak
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     x_l = torch.randint(0, 256, (Bl, 224, 224, 3), generator=g, dtype=torch.uint8).to(dev)

@@ -121,6 +121,22 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Stem BN -> ReLU -> max-pool, fused (torchvision bn1/relu/maxpool).
+ * Forward: out/idx = maxpool(T(relu(fma(y, scale, shift)))) without writing
+ * the full-resolution activation (bit-identical to ssip_bn_apply followed by
+ * ssip_maxpool_fwd).  Backward: dy = BN-backward of the ReLU-masked gathered
+ * pool gradient (replaces ssip_maxpool_bwd + ssip_bn_bwd); y is the pre-BN
+ * conv output [N][H][W][C]; partial sized by ..._partial_floats; coef 3*C.
+ * ---------------------------------------------------------------------- */
+int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
+                          const float* scale, const float* shift, void* out, uint8_t* idx, void* stream);
+int64_t ssip_stem_pool_bn_bwd_partial_floats(int N, int H, int W, int C);
+int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* dpool,
+                          const uint8_t* idx, const void* y, const float* mean, const float* invstd,
+                          const float* scale, const float* shift, const float* gamma, float* dgamma, float* dbeta,
+                          int accumulate, void* dy, float* partial, float* coef, void* stream);
+
+/* ------------------------------------------------------------------------
  * Pooling, head, losses
  * ---------------------------------------------------------------------- */
 int ssip_maxpool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* x, void* y,

@@ -50,6 +50,56 @@ def _view(img: Image.Image, size: int, degrees: float, strong: bool, g: torch.Ge
     return T.Normalize(MEAN, STD)(t)
 
 
+def view_from_draw(img: Image.Image, size: int, flip: bool, angle, brightness: float = 1.0, contrast: float = 1.0,
+                   cutout=None) -> torch.Tensor:
+    """One view with explicit per-sample parameters (what ssip's GPU
+    transform receives): Resize -> flip -> rotate(NEAREST) -> ToTensor ->
+    brightness/contrast (clamped) -> cutout (0.5) -> Normalize."""
+    img = img.resize((size, size), Image.BILINEAR) if img.size != (size, size) else img
+    if flip:
+        img = img.transpose(Image.FLIP_LEFT_RIGHT)
+    if angle is not None:
+        img = img.rotate(angle, Image.NEAREST, expand=False, fillcolor=(0, 0, 0))
+    t = T.ToTensor()(img)
+    if brightness != 1.0 or contrast != 1.0:
+        t = ((t * brightness - 0.5) * contrast + 0.5).clamp(0, 1)
+    if cutout is not None:
+        x0, y0, x1, y1 = cutout
+        t[:, y0:y1, x0:x1] = 0.5
+    return T.Normalize(MEAN, STD)(t)
+
+
+def semi_step_reference(model, opt, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.ndarray, draws_l, draws_w, draws_s,
+                        size: int, tau: float, lambda_u: float) -> torch.Tensor:
+    """One joint step with explicit view parameters (draws: (flip, angle,
+    brightness, contrast, cutout) tuples).  Returns [total, L_l, L_u, mask count]."""
+    xl = torch.stack([view_from_draw(Image.fromarray(a), size, *d) for a, d in zip(x_l, draws_l)])
+    xw = torch.stack([view_from_draw(Image.fromarray(a), size, *d) for a, d in zip(x_u, draws_w)])
+    xs = torch.stack([view_from_draw(Image.fromarray(a), size, *d) for a, d in zip(x_u, draws_s)])
+    dt = next(model.parameters()).dtype
+    xl, xw, xs = xl.to(dt), xw.to(dt), xs.to(dt)
+    bns = [b for b in model.modules() if isinstance(b, torch.nn.BatchNorm2d)]
+    model.train()
+    with torch.no_grad():
+        saved = [(b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone()) for b in bns]
+        zw = model(xw)
+        for b, (rm, rv, nb) in zip(bns, saved):
+            b.running_mean.copy_(rm)
+            b.running_var.copy_(rv)
+            b.num_batches_tracked.copy_(nb)
+    conf, pseudo = torch.softmax(zw, 1).max(1)
+    mask = (conf >= tau).to(dt)
+    opt.zero_grad(set_to_none=True)
+    z = model(torch.cat([xl, xs], 0))
+    Bl = xl.shape[0]
+    l_l = F.cross_entropy(z[:Bl], y_l)
+    l_u = (F.cross_entropy(z[Bl:], pseudo, reduction="none") * mask).mean()
+    loss = l_l + lambda_u * l_u
+    loss.backward()
+    opt.step()
+    return torch.stack([loss.detach(), l_l.detach(), l_u.detach(), mask.sum()])
+
+
 class CpuSemiStep:
     def __init__(self, seed: int = 42, tau: float = 0.7, lambda_u: float = 1.0, size: int = 224):
         torch.manual_seed(seed)

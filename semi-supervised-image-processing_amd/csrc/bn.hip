@@ -115,7 +115,7 @@ __global__ void bn_apply_kernel(int total8, int C, const T* __restrict__ y, cons
     if (res) r.load(res + (long)i * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float t = v.get(j) * sc[j] + sh[j];
+      float t = __builtin_fmaf(v.get(j), sc[j], sh[j]);  // the stem's fused kernels repeat this exactly
       if (res) t += r.get(j);
       if (relu) t = t > 0.f ? t : 0.f;
       o.set(j, t);

@@ -50,6 +50,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return f.mul ? (__umulhi(n, f.mul) >> f.shr) : n;
 }
 
+struct PhaseInfo {
+  int M, tiles_m, ksteps;     // rows (N * Hph * Wph), M-tiles, k-steps of this phase
+  int r0, s0, nr, ns, bh, bw;  // first tap, tap counts, dy offsets
+  int ph, pw, Wph;
+  FastDiv div_hw, div_w;       // / (Hph * Wph), / Wph
+};
+
 struct ConvArgs {
   int N, H, W, C, K, R, S, stride, pad, P, Q;
   int M;        // GEMM rows (FWD: N*P*Q, DGRAD: N*H*W, WGRAD: K)
@@ -71,6 +78,11 @@ struct ConvArgs {
   const void* py;
   const float* pmean;
   const float* pinvstd;
+  // DGRAD stride-2 phase split (LDS-DMA kernel): blockIdx.y = phase
+  // (ph, pw) = output rows h = 2i+ph, columns w = 2j+pw; only the taps
+  // r = r0 + 2*ri, s = s0 + 2*si reach them, at dy row p = i + bh - ri.
+  int phased;
+  PhaseInfo phase[4];
 };
 
 template <typename T> struct Traits;
@@ -323,10 +335,26 @@ __device__ __forceinline__ void dgrad_bn_post(const ConvArgs& a, char* smem, int
   }
 }
 
+// GEMM row -> output row (identity, or the phase's strided rows of dx)
+struct RowMap {
+  int M;
+  bool phased;  // false: identity
+  int H, W, ph, pw, Wph;
+  FastDiv div_hw, div_w;
+  __device__ __forceinline__ long row(int m) const {
+    if (!phased) return m;
+    const int n = fdiv(m, div_hw);
+    const int rem = m - n * (int)div_hw.d;
+    const int i = fdiv(rem, div_w);
+    const int j = rem - i * Wph;
+    return ((long)n * H + 2 * i + ph) * W + 2 * j + pw;
+  }
+};
+
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
                                                    int n0, int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
-                                                   bool pre_loaded) {
+                                                   bool pre_loaded, const RowMap& rmap) {
   constexpr int NT = 64 * WMW * WNW;
   constexpr int WTM = BM / WMW, WTN = BN / WNW;
   const int tid = threadIdx.x;
@@ -386,7 +414,8 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
     for (int id = tid; id < BM * CPR; id += NT) {
       const int row = id / CPR, ch = id % CPR;
       const int m = m0 + row, n = n0 + ch * 8;
-      if (m >= a.M || n >= a.Ng) continue;
+      if (m >= rmap.M || n >= a.Ng) continue;
+      const long orow = rmap.row(m);
       Vec8<T> v;
       const char* src = smem + row * EROW + ch * 8 * (int)sizeof(T);
       if constexpr (sizeof(T) == 2) {
@@ -399,12 +428,12 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
         if (Add) {
           // the unrounded accumulator would be better; the LDS copy is already in T
           Vec8<T> r;
-          r.load(Add + (long)m * a.Ng + n);
+          r.load(Add + orow * a.Ng + n);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v.set(j, v.get(j) + r.get(j));
         }
       }
-      v.store(Out + (long)m * a.Ng + n);
+      v.store(Out + orow * a.Ng + n);
     }
   }
 
@@ -485,13 +514,17 @@ template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
                                               int tm) {
   BnPostRegs<T, BM, BN, 64 * WMW * WNW> none;
-  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false);
+  RowMap rmap;
+  rmap.M = a.M;
+  rmap.phased = false;
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false, rmap);
 }
 
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
-                                              int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre) {
-  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, pre, true);
+                                              int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
+                                              const RowMap& rmap) {
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, pre, true, rmap);
 }
 
 // ---------------------------------------------------------------------------
@@ -823,6 +856,42 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   const int m0 = tm * BM, n0 = tn * BN;
   const T* __restrict__ Ag = static_cast<const T*>(a.A);
   const T* __restrict__ Bg = static_cast<const T*>(a.B);
+  // stride-2 DGRAD phase (uniform per workgroup); surplus M-tiles of the
+  // shorter phases leave before touching memory or a barrier
+  // (field-wise constant-index selects: a dynamic index into the kernel
+  // argument struct, or a pointer into a copy, lands it in scratch)
+  const bool phased = (MODE == MODE_DGRAD) && a.phased;
+  const int f = phased ? (int)blockIdx.y : 0;
+#define SSIP_PSEL(fld) \
+  (f == 0 ? a.phase[0].fld : f == 1 ? a.phase[1].fld : f == 2 ? a.phase[2].fld : a.phase[3].fld)
+  RowMap rmap;
+  rmap.phased = phased;
+  rmap.H = a.H;
+  rmap.W = a.W;
+  int ph_ns = a.S, ph_r0 = 0, ph_s0 = 0, ph_bh = 0, ph_bw = 0, ph_ksteps = a.ksteps;
+  if (phased) {
+    if (tm >= SSIP_PSEL(tiles_m)) return;
+    rmap.M = SSIP_PSEL(M);
+    rmap.ph = SSIP_PSEL(ph);
+    rmap.pw = SSIP_PSEL(pw);
+    rmap.Wph = SSIP_PSEL(Wph);
+    rmap.div_hw.d = SSIP_PSEL(div_hw.d);
+    rmap.div_hw.mul = SSIP_PSEL(div_hw.mul);
+    rmap.div_hw.shr = SSIP_PSEL(div_hw.shr);
+    rmap.div_w.d = SSIP_PSEL(div_w.d);
+    rmap.div_w.mul = SSIP_PSEL(div_w.mul);
+    rmap.div_w.shr = SSIP_PSEL(div_w.shr);
+    ph_ns = SSIP_PSEL(ns);
+    ph_r0 = SSIP_PSEL(r0);
+    ph_s0 = SSIP_PSEL(s0);
+    ph_bh = SSIP_PSEL(bh);
+    ph_bw = SSIP_PSEL(bw);
+    ph_ksteps = SSIP_PSEL(ksteps);
+  } else {
+    rmap.M = a.M;
+  }
+#undef SSIP_PSEL
+  const int Mrows = rmap.M;
 
   // ---------------- per-lane source state ----------------
   // FWD/DGRAD: instruction j = wave + NW*t covers k-tile rows 8j..8j+7;
@@ -843,7 +912,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       const int row = 8 * (wave + NW * t) + (lane >> 3);
       a_c[t] = (lane & 7) ^ ((row >> 1) & 7);
       const int m = m0 + row;
-      a_ok[t] = m < a.M;
+      a_ok[t] = m < Mrows;
       const int mm = a_ok[t] ? m : 0;
       if constexpr (MODE == MODE_FWD) {
         const int n = fdiv(mm, a.div_pq);
@@ -853,6 +922,14 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
         a_base[t] = n * a.H * a.W;
         a_h[t] = p * a.stride - a.pad;
         a_w[t] = q * a.stride - a.pad;
+      } else if (phased) {
+        const int n = fdiv(mm, rmap.div_hw);
+        const int rem = mm - n * (int)rmap.div_hw.d;
+        const int i = fdiv(rem, rmap.div_w);
+        const int j = rem - i * rmap.Wph;
+        a_base[t] = n * a.P * a.Q;
+        a_h[t] = i + ph_bh;  // dy row for tap ri: a_h - ri
+        a_w[t] = j + ph_bw;
       } else {
         const int n = fdiv(mm, a.div_hw);
         const int rem = mm - n * a.H * a.W;
@@ -929,7 +1006,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
         const int hp = a_h[t] - kr, wp = a_w[t] - ks_;
         int p = hp, q = wp;
         bool ok = a_ok[t] && hp >= 0 && wp >= 0;
-        if (a.stride != 1) {
+        if (!phased && a.stride != 1) {
           ok = ok && ((hp | wp) & (a.stride - 1)) == 0;
           p = hp >> (a.stride >> 1);
           q = wp >> (a.stride >> 1);
@@ -945,7 +1022,11 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       for (int t = 0; t < LB; ++t) {
         bool ok = b_ok[t];
         if constexpr (C4) ok = ok && ks * BK + b_c[t] * 8 < a.Kg;
-        const T* src = ok ? b_ptr[t] + ks * BK : reinterpret_cast<const T*>(g_zero16);
+        int koff = ks * BK;
+        if constexpr (MODE == MODE_DGRAD) {
+          if (phased) koff = ((ph_r0 + 2 * kr) * a.S + ph_s0 + 2 * ks_) * a.K + kcb;
+        }
+        const T* src = ok ? b_ptr[t] + koff : reinterpret_cast<const T*>(g_zero16);
         glds16(src, Bs + (wave + NW * t) * 1024);
       }
     } else {
@@ -977,7 +1058,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       kcb += BK;
       if (kcb >= Cred) {
         kcb = 0;
-        if (++ks_ >= a.S) { ks_ = 0; ++kr; }
+        if (++ks_ >= ph_ns) { ks_ = 0; ++kr; }
       }
     }
   };
@@ -988,7 +1069,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  int nsteps = a.ksteps;
+  int nsteps = ph_ksteps;
   if constexpr (WG) {
     const long rem = mend - mstart;
     nsteps = rem > 0 ? (int)((rem + BK - 1) / BK) : 0;
@@ -1032,7 +1113,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();
-  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post);
+  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -1330,6 +1411,39 @@ static int launch_conv(const Plan& pl, hipStream_t st) {
 
 static int elem_bytes_of(int dtype) { return dtype == SSIP_BF16 ? 2 : 4; }
 
+// Stride-2 DGRAD as four dense sub-problems, one per output parity phase:
+// phase (ph, pw) only meets the taps r = r0 + 2*ri, s = s0 + 2*si, so the
+// k-loop skips the 3/4 of (tap, pixel) pairs the plain implicit GEMM would
+// gather as zeros.  blockIdx.y = phase; grid.x covers the largest phase.
+static void phase_split(Plan& pl, const ssip_conv_desc* d) {
+  if (pl.stages == 0 || pl.conv1 || d->stride != 2) return;
+  const char* e = getenv("SSIP_CONV_NO_PHASE");
+  if (e && e[0] == '1') return;
+  ConvArgs& a = pl.args;
+  int max_tiles = 0;
+  for (int f = 0; f < 4; ++f) {
+    PhaseInfo& P = a.phase[f];
+    P.ph = f >> 1;
+    P.pw = f & 1;
+    const int Hph = (d->H - P.ph + 1) / 2, Wph = (d->W - P.pw + 1) / 2;
+    P.r0 = (P.ph + d->pad) % 2;
+    P.s0 = (P.pw + d->pad) % 2;
+    P.nr = P.r0 < d->R ? (d->R - P.r0 + 1) / 2 : 0;
+    P.ns = P.s0 < d->S ? (d->S - P.s0 + 1) / 2 : 0;
+    P.bh = (P.ph + d->pad - P.r0) / 2;
+    P.bw = (P.pw + d->pad - P.s0) / 2;
+    P.Wph = Wph;
+    P.M = d->N * Hph * Wph;
+    P.tiles_m = ceil_div(P.M, pl.bm);
+    P.ksteps = P.nr * P.ns * (d->K / 64);
+    P.div_hw = make_fastdiv((uint32_t)std::max(1, Hph * Wph));
+    P.div_w = make_fastdiv((uint32_t)std::max(1, Wph));
+    max_tiles = std::max(max_tiles, P.tiles_m);
+  }
+  a.phased = 1;
+  pl.grid = dim3(std::max(1, max_tiles) * a.tiles_n, 4, 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1364,6 +1478,7 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   Plan pl;
   int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
+  phase_split(pl, d);
   SSIP_REQUIRE(dy && w_crsk && dx, SSIP_ERR_ARG, "ssip_conv_dgrad: null pointer");
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));

@@ -241,6 +241,11 @@ class SSIPResNet(nn.Module):
             self._arena = ParamArena(list(self.parameters()))
         return self._arena
 
+    def prepare_weights(self, need_t: bool = True) -> None:
+        """Refresh the compute-dtype conv weight copies now (one launch) so a
+        later forward on another stream only reads them."""
+        _prepare_weights(self, need_t)
+
     # ------------------------------------------------------------------
     def forward(self, x):
         if isinstance(x, DeviceImages):
@@ -371,16 +376,14 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
     # stem: conv 7x7/2 -> BN -> ReLU -> maxpool 3x3/2
     rec = _conv_bn(model, model.conv1, model.bn1, images, N, H, W, train, save, upd, in_pad)
     g = rec.geom
-    z1 = torch.empty_like(rec.y)
-    ops.bn_apply(N * g.P * g.Q, g.K, rec.y, rec.stats[2], rec.stats[3], None, True, z1)
-    rec.z = z1
     mp = model.maxpool
     k, s, pd = mp.kernel_size, mp.stride, mp.padding
     Hp = (g.P + 2 * pd - k) // s + 1
     Wp = (g.Q + 2 * pd - k) // s + 1
     pool = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt)
     idx = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=torch.uint8)
-    ops.maxpool_fwd(N, g.P, g.Q, g.K, k, s, pd, z1, pool, idx)
+    # BN -> ReLU -> max-pool in one pass over y (the full-resolution z is never stored)
+    ops.stem_bn_pool_fwd(N, g.P, g.Q, g.K, k, s, pd, rec.y, rec.stats[2], rec.stats[3], pool, idx)
     if save:
         sv.stem, sv.pool_out, sv.pool_idx, sv.pool_hw = rec, pool, idx, (g.P, g.Q)
     x, Hc, Wc = pool, Hp, Wp
@@ -616,9 +619,14 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     stem = sv.stem
     P1, Q1 = sv.pool_hw
     mp = model.maxpool
-    dz1 = torch.empty_like(stem.y)
-    ops.maxpool_bwd(N, P1, Q1, stem.geom.K, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, dz1)
-    dy1 = bn_backward(stem, dz1, stem.z)
+    # max-pool backward + ReLU mask + BN backward straight from the pooled gradient
+    C1 = stem.geom.K
+    dgam, dbet, acc = bn_grads(stem)
+    dy1 = torch.empty_like(stem.y)
+    partial = torch.empty(ops.stem_pool_bn_bwd_partial_floats(N, P1, Q1, C1), device=dev, dtype=torch.float32)
+    ops.stem_pool_bn_bwd(N, P1, Q1, C1, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, stem.y,
+                         stem.stats[0], stem.stats[1], stem.stats[2], stem.stats[3], stem.bn.weight.detach(), dgam,
+                         dbet, acc, dy1, partial, coef_buf[: 3 * C1])
     conv_wgrad(stem, dy1)
     if hook is not None:
         hook([model.conv1.weight, model.bn1.weight, model.bn1.bias])

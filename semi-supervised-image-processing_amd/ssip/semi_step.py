@@ -12,7 +12,8 @@ itself trains offline pseudo-labels, it has no joint step):
 Step (per rank, B_l labelled + B_u unlabelled uint8 images resident in HBM):
   1. GPU augment: weak(labelled), weak(unlabelled), strong(unlabelled)
   2. weak forward over the unlabelled weak view: train-mode BN batch
-     statistics, no running-stat update, no grad (pseudo-label source)
+     statistics, no running-stat update, no grad (pseudo-label source),
+     on a second HIP stream, overlapping step 3
   3. one train forward over [labelled ; strong] (B_l + B_u images)
   4. ssip_semi_loss: CE(labelled) + lambda * mean_u[mask * CE(strong, pseudo)]
   5. backward (+ bucketed RCCL all-reduce when world > 1)
@@ -49,6 +50,13 @@ class SemiStep:
         self.gen = torch.Generator().manual_seed(seed)
         if bucketer is not None:
             model.grad_ready_hook = bucketer.mark_ready
+        self.overlap = True   # weak forward on a second HIP stream
+        self._side = None
+
+    def _side_stream(self, dev):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=dev)
+        return self._side
 
     def draw_params(self, Bl: int, Bu: int):
         """Per-sample view parameters (host RNG, like a DataLoader worker)."""
@@ -65,24 +73,33 @@ class SemiStep:
         if params is None:
             params = self.draw_params(Bl, Bu)
         pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
-        # 1. views: [labelled weak ; unlabelled strong] in one buffer, weak unlabelled separately
+        main = torch.cuda.current_stream(dev)
         S = self.size
         P = self.tf.pad
+        m.train()
+        # compute-dtype weights for both forwards, refreshed once, before the fork
+        m.prepare_weights(need_t=True)
+        # 2. weak view + weak forward on a side stream (batch-stat BN, no
+        #    running update, no grad): it only meets the train forward at the
+        #    loss, so the two latency-bound forwards overlap on the chip
+        side = self._side_stream(dev) if self.overlap else main
+        side.wait_stream(main)
+        m.bn_update_running = False
+        with torch.cuda.stream(side), torch.no_grad():
+            xw = self.tf(x_u, pw)
+            zw = m(xw)
+        m.bn_update_running = True
+        # 1+3. [labelled weak ; unlabelled strong] views and the joint train forward
         x_ls = torch.empty((Bl + Bu, S + 2 * P, S + 2 * P, 4), device=dev, dtype=m.compute_dtype)
         self.tf(x_l, pl, out=x_ls[:Bl])
         self.tf(x_u, ps, out=x_ls[Bl:])
-        xw = self.tf(x_u, pw)
-        # 2. weak forward: batch-stat BN, no running update, no grad
-        m.train()
-        m.bn_update_running = False
-        with torch.no_grad():
-            zw = m(xw)
-        m.bn_update_running = True
-        # 3. joint train forward
         self.opt.zero_grad(set_to_none=True)
         if self.bucketer is not None:
             self.bucketer.reset()
         logits = m(DeviceImages(x_ls, P))
+        if side is not main:
+            main.wait_stream(side)
+            zw.record_stream(main)
         # 4. loss + dlogits in one launch
         out, dzl, dzs, pseudo, mask = ops.semi_loss(logits[:Bl].detach().contiguous(), y_l,
                                                     zw.contiguous(), logits[Bl:].detach().contiguous(),

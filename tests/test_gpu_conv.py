@@ -16,6 +16,7 @@ SHAPES = [
     (2, 64, 16, 16, 64, 3, 1, 1),
     (2, 64, 16, 16, 128, 3, 2, 1),
     (2, 128, 15, 15, 256, 1, 2, 0),
+    (2, 64, 15, 13, 128, 3, 2, 1),  # odd H/W: unequal stride-2 dgrad phases
     (3, 64, 7, 7, 192, 3, 1, 1),
     (2, 3, 32, 32, 64, 7, 2, 3),   # stem (C padded to 4, S to 8)
     (1, 256, 7, 7, 512, 3, 1, 1),

@@ -255,3 +255,58 @@ def test_weight_cache_follows_optimizer(dev):
     exp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
     assert torch.equal(m._prep[key][0], exp)
     assert not torch.equal(before, exp)
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_stem_bn_pool_fused_matches_unfused(dev, dtname):
+    """Fused stem BN->ReLU->max-pool forward is bit-identical to bn_apply +
+    maxpool_fwd (values and argmax bytes); the fused backward matches
+    maxpool_bwd + bn_bwd (f32 1e-5, bf16 2e-2: the unfused path rounds the
+    scattered gradient to bf16 before the BN backward, the fused one keeps f32)."""
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    torch.manual_seed(0)
+    N, H, W, C, k, s, pd = 3, 20, 18, 64, 3, 2, 1
+    M = N * H * W
+    y = torch.randn(N, H, W, C, device=dev).to(dt)
+    mean = torch.randn(C, device=dev) * 0.1
+    invstd = torch.rand(C, device=dev) + 0.5
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.1
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    P, Q = (H + 2 * pd - k) // s + 1, (W + 2 * pd - k) // s + 1
+    # unfused reference path
+    z = torch.empty_like(y)
+    ops.bn_apply(M, C, y, scale, shift, None, True, z)
+    pool_r = torch.empty(N, P, Q, C, device=dev, dtype=dt)
+    idx_r = torch.empty(N, P, Q, C, device=dev, dtype=torch.uint8)
+    ops.maxpool_fwd(N, H, W, C, k, s, pd, z, pool_r, idx_r)
+    # fused
+    pool = torch.empty_like(pool_r)
+    idx = torch.empty_like(idx_r)
+    ops.stem_bn_pool_fwd(N, H, W, C, k, s, pd, y, scale, shift, pool, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(pool.cpu(), pool_r.cpu())
+    assert torch.equal(idx.cpu(), idx_r.cpu())
+    # backward
+    dpool = torch.randn(N, P, Q, C, device=dev).to(dt)
+    dz = torch.empty_like(y)
+    ops.maxpool_bwd(N, H, W, C, k, s, pd, dpool, idx_r, dz)
+    dy_r = torch.empty_like(y)
+    dg_r = torch.empty(C, device=dev)
+    db_r = torch.empty(C, device=dev)
+    part = torch.empty(ops.bn_bwd_partial_floats(M, C), device=dev)
+    coef = torch.empty(3 * C, device=dev)
+    ops.bn_bwd(M, C, dz, z, y, mean, invstd, gamma, dg_r, db_r, False, dy_r, None, part, coef)
+    dy = torch.empty_like(y)
+    dg = torch.empty(C, device=dev)
+    db = torch.empty(C, device=dev)
+    part2 = torch.empty(ops.stem_pool_bn_bwd_partial_floats(N, H, W, C), device=dev)
+    coef2 = torch.empty(3 * C, device=dev)
+    ops.stem_pool_bn_bwd(N, H, W, C, k, s, pd, dpool, idx, y, mean, invstd, scale, shift, gamma, dg, db, False, dy,
+                         part2, coef2)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    assert _rel(dy, dy_r) < tol
+    assert _rel(dg, dg_r) < tol
+    assert _rel(db, db_r) < tol

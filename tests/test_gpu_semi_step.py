@@ -1,0 +1,81 @@
+"""GPU parity of the benchmarked workload, ssip.semi_step.SemiStep (GPU views,
+weak forward on a side stream, joint forward/backward, fused consistency
+loss, fused AdamW), against oracle.step_oracle.semi_step_reference run in
+float64 on the CPU with the same images and per-sample view parameters.
+
+Tolerances (fp32 engine): loss terms rel 1e-4, mask count exact, gradients
+cos > 0.9999 (ReLU-mask flips near zero, see test_gpu_resnet.py), first AdamW
+update (~lr * sign(g)) mean |difference| < 1 % of lr per tensor."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.step_oracle import semi_step_reference
+from oracle.torchvision_restate.torchvision import models as tvm
+from ssip import SSIPResNet, replace_fc
+from ssip.augment import draw_strong_params, draw_train_params, encode_params
+from ssip.semi_step import SemiStep
+
+pytestmark = pytest.mark.gpu
+
+
+def _cos(a, b):
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return (a @ b / (a.norm() * b.norm()).clamp_min(1e-30)).item()
+
+
+def _tuple(d):
+    return (d.flip, d.angle, d.brightness, d.contrast, d.cutout)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_semi_step_matches_oracle(dev, overlap):
+    S, Bl, Bu, tau, lr = 64, 4, 4, 0.5, 1e-4
+    rng = np.random.default_rng(0)
+    x_l = rng.integers(0, 256, (Bl, S, S, 3), dtype=np.uint8)
+    x_u = rng.integers(0, 256, (Bu, S, S, 3), dtype=np.uint8)
+    y_l = torch.tensor([0, 1, 1, 0])
+    g = torch.Generator().manual_seed(7)
+    dl = [draw_train_params(10.0, g) for _ in range(Bl)]
+    dw = [draw_train_params(10.0, g) for _ in range(Bu)]
+    ds = [draw_strong_params(S, g) for _ in range(Bu)]
+
+    torch.manual_seed(0)
+    ref = tvm.resnet18()
+    ref.fc = torch.nn.Linear(512, 2)
+    torch.manual_seed(0)
+    mine = SSIPResNet("resnet18", num_classes=1000, dtype="fp32")
+    replace_fc(mine, 2)
+    ref64 = copy.deepcopy(ref).double()
+    p0 = {k: v.detach().clone() for k, v in ref64.named_parameters()}
+    opt = torch.optim.AdamW(ref64.parameters(), lr=lr, weight_decay=1e-4)
+    out_ref = semi_step_reference(ref64, opt, x_l, y_l, x_u, [_tuple(d) for d in dl], [_tuple(d) for d in dw],
+                                  [_tuple(d) for d in ds], S, tau, 1.0)
+
+    mine = mine.to(dev)
+    step = SemiStep(mine, lr=lr, weight_decay=1e-4, tau=tau, lambda_u=1.0, image_size=S)
+    step.overlap = overlap
+    params = (encode_params(dl, S, S), encode_params(dw, S, S), encode_params(ds, S, S))
+    st = step(torch.from_numpy(x_l).to(dev), y_l.to(dev), torch.from_numpy(x_u).to(dev), params)
+    torch.cuda.synchronize()
+    out = st.loss.cpu().double()
+    assert out[3].item() == out_ref[3].item()
+    for i in range(3):
+        assert abs(out[i].item() - out_ref[i].item()) <= 1e-4 * max(1.0, abs(out_ref[i].item())), i
+    named = dict(mine.named_parameters())
+    for k, pr in ref64.named_parameters():
+        gm = step.arena.grad_view(named[k])
+        assert _cos(gm, pr.grad) > 0.9999, k
+        dmine = named[k].detach().double().cpu() - p0[k]
+        dref = pr.detach() - p0[k]
+        assert (dmine - dref).abs().mean().item() < 0.01 * lr, k
+    # BN running statistics: updated once (joint forward), not by the weak forward
+    for (n1, b1), (n2, b2) in zip(ref64.named_buffers(), mine.named_buffers()):
+        assert n1 == n2
+        if b1.dtype.is_floating_point:
+            assert ((b2.double().cpu() - b1).abs().max() / b1.abs().max().clamp_min(1e-12)).item() < 1e-4, n1
+        else:
+            assert torch.equal(b1, b2.cpu()), n1

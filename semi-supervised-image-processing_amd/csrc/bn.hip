@@ -17,67 +17,75 @@
 // dy = A*dout + B*y + Cc  (per-channel A, B, Cc) and optionally dout itself
 // (the gradient that flows down the identity branch).
 #include "ssip_common.h"
+#include "bn_common.h"
 
 namespace {
 
-__global__ void bn_finalize_kernel(int C, int tiles, const float* __restrict__ partial, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* running_mean, float* running_var,
-                                   float momentum, float eps, int update_running, float* mean_out,
-                                   float* invstd_out, float* scale_out, float* shift_out) {
+// One workgroup (1024 threads) per channel, one pass over the per-tile
+// {count, sum, M2} records: each thread folds its tiles with Chan's parallel
+// update in fp64, then a fixed-order tree merges the 1024 partial states.
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
+  const double nn = n + nb;
+  if (nn <= 0.0) return;
+  const double d = meanb - mean;
+  mean += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(int C, int tiles, const float* __restrict__ partial,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* running_mean,
+                                                           float* running_var, float momentum, float eps,
+                                                           int update_running, float* mean_out, float* invstd_out,
+                                                           float* scale_out, float* shift_out) {
   const int c = blockIdx.x;
-  __shared__ double red[256];
-  __shared__ double s_mean, s_n;
-  double n = 0.0, sum = 0.0;
-  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
-    const float* rec = partial + ((long)c * tiles + t) * 3;
-    n += rec[0];
-    sum += rec[1];
+  __shared__ double sn[1024], sm[1024], s2[1024];
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  const float* rec = partial + (long)c * tiles * 3;
+  int t = threadIdx.x;
+  // 4 records in flight per thread
+  for (; t + 3 * 1024 < tiles; t += 4 * 1024) {
+    float r[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) r[u][v] = rec[(long)(t + u * 1024) * 3 + v];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (r[u][0] > 0.f) chan_merge(n, mean, m2, r[u][0], (double)r[u][1] / r[u][0], r[u][2]);
   }
-  // reduce n
-  red[threadIdx.x] = n;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
+  for (; t < tiles; t += 1024) {
+    const float nb = rec[(long)t * 3], sb = rec[(long)t * 3 + 1], mb = rec[(long)t * 3 + 2];
+    if (nb > 0.f) chan_merge(n, mean, m2, nb, (double)sb / nb, mb);
   }
-  if (threadIdx.x == 0) s_n = red[0];
+  sn[threadIdx.x] = n;
+  sm[threadIdx.x] = mean;
+  s2[threadIdx.x] = m2;
   __syncthreads();
-  red[threadIdx.x] = sum;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) s_mean = red[0] / s_n;
-  __syncthreads();
-  const double mean = s_mean, N = s_n;
-  double m2 = 0.0;
-  for (int t = threadIdx.x; t < tiles; t += blockDim.x) {
-    const float* rec = partial + ((long)c * tiles + t) * 3;
-    const double nt = rec[0];
-    if (nt > 0) {
-      const double d = (double)rec[1] / nt - mean;
-      m2 += (double)rec[2] + nt * d * d;
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      double a = sn[threadIdx.x], am = sm[threadIdx.x], a2 = s2[threadIdx.x];
+      chan_merge(a, am, a2, sn[threadIdx.x + o], sm[threadIdx.x + o], s2[threadIdx.x + o]);
+      sn[threadIdx.x] = a;
+      sm[threadIdx.x] = am;
+      s2[threadIdx.x] = a2;
     }
-  }
-  red[threadIdx.x] = m2;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double var = red[0] / N;
+    const double N = sn[0], mu = sm[0];
+    const double var = s2[0] / N;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
     const float scale = g * invstd;
-    mean_out[c] = (float)mean;
+    mean_out[c] = (float)mu;
     invstd_out[c] = invstd;
     scale_out[c] = scale;
-    shift_out[c] = b - (float)mean * scale;
+    shift_out[c] = b - (float)mu * scale;
     if (update_running) {
-      const double unbiased = N > 1 ? red[0] / (N - 1) : var;
-      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      const double unbiased = N > 1 ? s2[0] / (N - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
     }
   }
@@ -183,42 +191,6 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(int C, int blocks, long M, const float* __restrict__ partial,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ invstd, float* dgamma, float* dbeta,
-                                       int accumulate, float* coef) {
-  const int c = blockIdx.x;
-  __shared__ double r0[256], r1[256];
-  double a = 0.0, b = 0.0;
-  for (int t = threadIdx.x; t < blocks; t += blockDim.x) {
-    a += partial[((long)t * C + c) * 2 + 0];
-    b += partial[((long)t * C + c) * 2 + 1];
-  }
-  r0[threadIdx.x] = a;
-  r1[threadIdx.x] = b;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      r0[threadIdx.x] += r0[threadIdx.x + o];
-      r1[threadIdx.x] += r1[threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const double sum_d = r0[0], sum_dx = r1[0];
-    if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + sum_dx : sum_dx);
-    if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + sum_d : sum_d);
-    const double g = gamma ? gamma[c] : 1.0;
-    const double is = invstd[c];
-    const double A = g * is;
-    const double k0 = -A * sum_d / (double)M;
-    const double k1 = -A * sum_dx / (double)M * is;
-    coef[c] = (float)A;                       // * dout
-    coef[C + c] = (float)k1;                  // * y
-    coef[2 * C + c] = (float)(k0 - k1 * mean[c]);  // constant
-  }
-}
-
 template <typename T>
 __global__ void bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz, const T* __restrict__ zmask,
                                     const T* __restrict__ y, const float* __restrict__ coef, T* __restrict__ dy,
@@ -286,7 +258,7 @@ int ssip_bn_finalize(int C, int tiles, const float* partial, const float* gamma,
   SSIP_REQUIRE(C > 0 && tiles > 0 && partial && mean_out && invstd_out && scale_out && shift_out, SSIP_ERR_ARG,
                "ssip_bn_finalize: bad arguments");
   SSIP_REQUIRE(!update_running || (running_mean && running_var), SSIP_ERR_ARG, "running stats required");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, C, tiles, partial, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(1024), 0, (hipStream_t)stream, C, tiles, partial, gamma, beta,
                      running_mean, running_var, momentum, eps, update_running, mean_out, invstd_out, scale_out,
                      shift_out);
   return ::ssip::check_launch("bn_finalize");
@@ -333,7 +305,7 @@ int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, 
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, (const T*)y, mean, invstd, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, C, blocks, (long)M, partial, gamma, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, blocks, (long)M, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
                        (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre);
@@ -350,7 +322,7 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                "ssip_bn_bwd_from_partials: unsupported size");
   hipStream_t st = (hipStream_t)stream;
   const int total8 = (int)(M * C / 8);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, C, tiles, (long)M, partial, gamma, mean,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, tiles, (long)M, partial, gamma, mean,
                      invstd, dgamma, dbeta, accumulate, coef);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dout,

@@ -110,6 +110,15 @@ def main():
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
 
+    # HBM traffic of the same family from the committed rocprofv3 PMC passes of
+    # this workload (tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE, separate
+    # passes, per step) — counters cannot be read from inside the run itself
+    traffic = None
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("conv", {}).get("total_bytes")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.step_oracle import time_cpu_step
@@ -142,7 +151,9 @@ def main():
                        "gflop_per_step_per_gpu": round(Bl * GFLOP_PER_IMG_TRAIN + Bu * (GFLOP_PER_IMG_FWD
                                                                                         + GFLOP_PER_IMG_TRAIN), 1)},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "traffic_note": "bytes per step for the same conv family, PMC FETCH_SIZE*2 + WRITE_SIZE "
+                                         "(profiles/r1_pmc_traffic.json; Infinity-Cache hits are counted)",
                          "kernel": "conv_glds_kernel + conv_gemm_kernel (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
                                    f"in {conv_ms:.3f} ms"},

@@ -141,7 +141,7 @@ __device__ __forceinline__ void pool_rows(int h, int P, int k, int s, int pad, i
 // [blocks][C][2] as ssip_bn_bwd's reduction.  A workgroup owns `rows`
 // consecutive (n, h) rows of the full-resolution map.
 template <typename T>
-__global__ void __launch_bounds__(256) stem_pool_bn_bwd_reduce_kernel(
+__global__ void __launch_bounds__(128) stem_pool_bn_bwd_reduce_kernel(
     int N, int H, int W, int C, int P, int Q, int k, int s, int pad, int rows, const T* __restrict__ dpool,
     const uint8_t* __restrict__ idx, const T* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256) stem_pool_bn_bwd_reduce_kernel(
       }
     }
   }
-  __shared__ float red[2][256][9];
+  __shared__ float red[2][128][9];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     red[0][threadIdx.x][j] = sd[j];
@@ -243,9 +243,9 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_apply_kernel(
   }
 }
 
-// full-resolution rows (n, h) per reduction workgroup: ~1024 workgroups
+// full-resolution rows (n, h) per reduction workgroup: ~2048 workgroups
 static int rows_per_block(int N, int H) {
-  const int rows = (N * H + 1023) / 1024;
+  const int rows = (N * H + 2047) / 2048;
   return rows < 1 ? 1 : rows;
 }
 
@@ -287,7 +287,7 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   const int blocks = (N * H + rows - 1) / rows;
   hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, N, H, W, C, P, Q, k, s,
+    hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                        pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, blocks, M, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);

@@ -1,0 +1,44 @@
+"""HBM traffic per train step from rocprofv3 PMC passes (MI355X_MICROARCH.md
+HBM section): FETCH_SIZE and WRITE_SIZE collected in SEPARATE runs (they do
+not fit one TCC pass); FETCH_SIZE doubled (gfx950 tallies 128-B requests at
+64 B); values are KiB per dispatch.
+
+usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json]
+Groups dispatches of the last complete step (between the last two AdamW
+launches) by kernel family and prints bytes per step.
+"""
+import collections, csv, json, sys
+
+
+def family(n):
+    for k in ("conv_gemm_kernel", "conv_glds_kernel"):
+        if k in n:
+            return "conv"
+    if "wgrad_reduce" in n:
+        return "conv"  # the wgrad split-K reduce belongs to the conv family (as in bench.py's roofline)
+    for k in ("stem_", "bn_", "maxpool", "augment", "adamw", "avgpool", "weight_prep", "semi_loss"):
+        if k in n:
+            return k.rstrip("_")
+    return "other"
+
+
+def per_step(path, counter):
+    rows = [r for r in csv.DictReader(open(path)) if r.get("Counter_Name", counter) == counter]
+    idx = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
+    a, b = idx[-2], idx[-1]
+    fam = collections.Counter()
+    for r in rows[a + 1:b + 1]:
+        fam[family(r["Kernel_Name"])] += float(r["Counter_Value"]) * 1024.0
+    return fam
+
+
+fetch = per_step(sys.argv[1], "FETCH_SIZE")
+write = per_step(sys.argv[2], "WRITE_SIZE")
+out = {}
+for k in sorted(set(fetch) | set(write)):
+    rd = 2.0 * fetch.get(k, 0.0)
+    wr = write.get(k, 0.0)
+    out[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr}
+    print(f"{k:12s} read {rd / 1e9:8.3f} GB  write {wr / 1e9:8.3f} GB  total {(rd + wr) / 1e9:8.3f} GB per step")
+if len(sys.argv) > 3:
+    json.dump(out, open(sys.argv[3], "w"), indent=1)

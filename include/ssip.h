@@ -112,6 +112,12 @@ int64_t ssip_bn_bwd_partial_floats(int64_t M, int C);
 int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
                 const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
                 void* dpre, float* partial, float* coef, void* stream);
+/* ssip_bn_bwd for a BN+ReLU without residual: the ReLU mask is recomputed
+ * from y as fma(y, scale, shift) > 0 (bit-identical to ssip_bn_apply's
+ * output sign), so the activation z is never read. */
+int ssip_bn_relu_bwd(int dtype, int64_t M, int C, const void* dz, const void* y, const float* mean,
+                     const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
+                     float* dbeta, int accumulate, void* dy, float* partial, float* coef, void* stream);
 /* Finish a BN backward whose reduction came from ssip_conv_dgrad_bn's partials
  * ([tiles][C][2] sums of dout and dout*xhat; dout already ReLU-masked):
  * dgamma/dbeta (+)= ..., dy = dBN(dout). */

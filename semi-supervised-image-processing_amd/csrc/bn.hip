@@ -138,6 +138,7 @@ template <typename T>
 __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T* __restrict__ dz,
                                      const T* __restrict__ zmask, const T* __restrict__ y,
                                      const float* __restrict__ mean, const float* __restrict__ invstd,
+                                     const float* __restrict__ mscale, const float* __restrict__ mshift,
                                      float* __restrict__ partial) {
   const int cpr = C / 8;               // chunks per row
   const int rpi = 256 / cpr;           // rows per iteration (>= 1 since C <= 2048)
@@ -147,10 +148,13 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
   const long r0 = (long)blockIdx.x * rows_per_block;
   long r1 = r0 + rows_per_block;
   if (r1 > M) r1 = M;
-  float sd[8], sx[8], mu[8], is[8];
+  float sd[8], sx[8], mu[8], is[8], msc[8], msh[8];
+  const bool amask = mscale != nullptr;  // ReLU mask recomputed from y (no z read)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sd[j] = 0.f; sx[j] = 0.f; mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j];
+    msc[j] = amask ? mscale[c0 + j] : 0.f;
+    msh[j] = amask ? mshift[c0 + j] : 0.f;
   }
   if (rsub < rpi) {
     for (long r = r0 + rsub; r < r1; r += rpi) {
@@ -162,6 +166,7 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
       for (int j = 0; j < 8; ++j) {
         float d = g.get(j);
         if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
+        if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
         const float xh = (yy.get(j) - mu[j]) * is[j];
         sd[j] += d;
         sx[j] += d * xh;
@@ -194,13 +199,19 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
 template <typename T>
 __global__ void bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz, const T* __restrict__ zmask,
                                     const T* __restrict__ y, const float* __restrict__ coef, T* __restrict__ dy,
-                                    T* __restrict__ dpre) {
+                                    T* __restrict__ dpre, const float* __restrict__ mscale,
+                                    const float* __restrict__ mshift) {
   const int cpr = C >> 3;
   const int start = blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (start % cpr) * 8;
-  float ca[8], cb[8], cc[8];
+  float ca[8], cb[8], cc[8], msc[8], msh[8];
+  const bool amask = mscale != nullptr;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j]; }
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j];
+    msc[j] = amask ? mscale[c0 + j] : 0.f;
+    msh[j] = amask ? mshift[c0 + j] : 0.f;
+  }
   const int stride = gridDim.x * blockDim.x;
   for (int i = start; i < total8; i += stride) {
     Vec8<T> g, zz, yy, o, p;
@@ -211,6 +222,7 @@ __global__ void bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz,
     for (int j = 0; j < 8; ++j) {
       float d = g.get(j);
       if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
+      if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
       p.set(j, d);
       o.set(j, ca[j] * d + cb[j] * yy.get(j) + cc[j]);
     }
@@ -292,9 +304,10 @@ int64_t ssip_bn_bwd_partial_floats(int64_t M, int C) {
   return ((M + rows - 1) / rows) * (int64_t)C * 2;
 }
 
-int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
-                const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
-                void* dpre, float* partial, float* coef, void* stream) {
+static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* zmask, const float* mscale,
+                       const float* mshift, const void* y, const float* mean, const float* invstd,
+                       const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy, void* dpre,
+                       float* partial, float* coef, void* stream) {
   SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= 2048 && dz && y && mean && invstd && dy && partial && coef,
                SSIP_ERR_ARG, "ssip_bn_bwd: bad arguments");
   hipStream_t st = (hipStream_t)stream;
@@ -304,11 +317,11 @@ int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, 
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
-                       (const T*)zmask, (const T*)y, mean, invstd, partial);
+                       (const T*)zmask, (const T*)y, mean, invstd, mscale, mshift, partial);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, blocks, (long)M, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
-                       (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre);
+                       (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
 }
@@ -326,9 +339,25 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                      invstd, dgamma, dbeta, accumulate, coef);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
-                       (const T*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr);
+                       (const T*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr);
   });
   return ::ssip::check_launch("bn_bwd_from_partials");
+}
+
+int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
+                const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
+                void* dpre, float* partial, float* coef, void* stream) {
+  return bn_bwd_impl(dtype, M, C, dz, zmask, nullptr, nullptr, y, mean, invstd, gamma, dgamma, dbeta, accumulate, dy,
+                     dpre, partial, coef, stream);
+}
+
+int ssip_bn_relu_bwd(int dtype, int64_t M, int C, const void* dz, const void* y, const float* mean,
+                     const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
+                     float* dbeta, int accumulate, void* dy, float* partial, float* coef, void* stream) {
+  SSIP_REQUIRE(scale && shift, SSIP_ERR_ARG, "ssip_bn_relu_bwd: scale/shift required");
+  return bn_bwd_impl(dtype, M, C, dz, nullptr, scale, shift, y, mean, invstd, gamma, dgamma, dbeta, accumulate, dy,
+                     nullptr, partial, coef, stream);
 }
 
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream) {

@@ -1281,7 +1281,9 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
     const int total_ks = ceil_div(a.Mred, BK);
     // ~1024 blocks (4 per CU), slab <= 64 MiB (stays in the Infinity Cache),
     // >= 16 k-steps per split (keeps the slab and its reduction small)
-    int splits = ceil_div(1024, tiles);
+    int target = 1024;
+    if (const char* e = getenv("SSIP_WGRAD_BLOCKS")) target = std::max(1, atoi(e));  // tuning override
+    int splits = ceil_div(target, tiles);
     const long slab_split = (long)a.M * a.Ng * 4;
     const int cap_bytes = (int)std::max<long>(1, (64l << 20) / slab_split);
     if (splits > cap_bytes) splits = cap_bytes;

@@ -76,6 +76,7 @@ _SIGS = {
     "ssip_bn_apply": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "ssip_bn_bwd_partial_floats": (_c_i64, [_c_i64, _c_int]),
     "ssip_bn_bwd": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_bn_relu_bwd": (_c_int, [_c_int, _c_i64, _c_int] + [_vp] * 9 + [_c_int, _vp, _vp, _vp, _vp]),
     "ssip_bn_bwd_from_partials": (_c_int, [_c_int, _c_i64, _c_int, _c_int] + [_vp] * 8 + [_c_int, _vp, _vp, _vp]),
     "ssip_relu_bwd": (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp]),
     "ssip_stem_bn_pool_fwd": (_c_int, [_c_int] * 8 + [_vp] * 6),

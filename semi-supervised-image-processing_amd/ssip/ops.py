@@ -250,6 +250,13 @@ def bn_bwd(M: int, C: int, dz, zmask, y, mean, invstd, gamma, dgamma, dbeta, acc
          _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(dpre), _p(partial), _p(coef), stream_ptr())
 
 
+def bn_relu_bwd(M: int, C: int, dz, y, mean, invstd, scale, shift, gamma, dgamma, dbeta, accumulate: bool, dy,
+                partial, coef) -> None:
+    """BN+ReLU backward with the mask recomputed from y (no z read)."""
+    call("ssip_bn_relu_bwd", dtype_code(dz), M, C, _p(dz), _p(y), _p(mean), _p(invstd), _p(scale), _p(shift),
+         _p(gamma), _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(partial), _p(coef), stream_ptr())
+
+
 def bn_bwd_from_partials(M: int, C: int, tiles: int, partial, dout, y, mean, invstd, gamma, dgamma, dbeta,
                          accumulate: bool, dy, coef) -> None:
     call("ssip_bn_bwd_from_partials", dtype_code(dout), M, C, tiles, _p(partial), _p(dout), _p(y), _p(mean),

@@ -528,6 +528,18 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
                    dy, dpre, partial, coef_buf[: 3 * g.K])
         return dy
 
+    def bn_relu_backward(rec: _ConvRec, dzin):
+        """BN+ReLU (no residual) backward; the mask comes from y and the BN
+        affine, so z is not read."""
+        g = rec.geom
+        M = N * g.P * g.Q
+        dgam, dbet, acc = bn_grads(rec)
+        dy = torch.empty_like(rec.y)
+        partial = torch.empty(ops.bn_bwd_partial_floats(M, g.K), device=dev, dtype=torch.float32)
+        ops.bn_relu_bwd(M, g.K, dzin, rec.y, rec.stats[0], rec.stats[1], rec.stats[2], rec.stats[3],
+                        rec.bn.weight.detach(), dgam, dbet, acc, dy, partial, coef_buf[: 3 * g.K])
+        return dy
+
     def bn_backward_fused(rec: _ConvRec, dpre, partial, tiles):
         """BN backward whose reduction came out of the dgrad epilogue that
         produced dpre (already ReLU-masked)."""
@@ -592,7 +604,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
                 dzp = torch.empty_like(r.x)
                 fused = conv_dgrad_bn(r, g_cur, recs[i - 1], dzp)
                 if fused is None:
-                    g_cur = bn_backward(recs[i - 1], dzp, recs[i - 1].z)
+                    g_cur = bn_relu_backward(recs[i - 1], dzp)
                 else:
                     g_cur = bn_backward_fused(recs[i - 1], *fused)
             elif need_dx:

@@ -310,3 +310,37 @@ def test_stem_bn_pool_fused_matches_unfused(dev, dtname):
     assert _rel(dy, dy_r) < tol
     assert _rel(dg, dg_r) < tol
     assert _rel(db, db_r) < tol
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_bn_relu_bwd_affine_mask_matches_z_mask(dev, dtname):
+    """ssip_bn_relu_bwd (mask from fma(y, scale, shift) > 0) is bit-identical to
+    ssip_bn_bwd with the stored ReLU output as the mask."""
+    dt = torch.float32 if dtname == "f32" else torch.bfloat16
+    torch.manual_seed(1)
+    M, C = 3000, 128
+    y = torch.randn(M, C, device=dev).to(dt)
+    dz = torch.randn(M, C, device=dev).to(dt)
+    mean = torch.randn(C, device=dev) * 0.1
+    invstd = torch.rand(C, device=dev) + 0.5
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.1
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    z = torch.empty_like(y)
+    ops.bn_apply(M, C, y, scale, shift, None, True, z)
+    outs = []
+    for affine in (False, True):
+        dy = torch.empty_like(y)
+        dg = torch.empty(C, device=dev)
+        db = torch.empty(C, device=dev)
+        part = torch.empty(ops.bn_bwd_partial_floats(M, C), device=dev)
+        coef = torch.empty(3 * C, device=dev)
+        if affine:
+            ops.bn_relu_bwd(M, C, dz, y, mean, invstd, scale, shift, gamma, dg, db, False, dy, part, coef)
+        else:
+            ops.bn_bwd(M, C, dz, z, y, mean, invstd, gamma, dg, db, False, dy, None, part, coef)
+        outs.append((dy.cpu(), dg.cpu(), db.cpu()))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -8,8 +8,10 @@
  * reaches at the cited call site (paths relative to the reference repo):
  *
  *   model(inputs) / loss.backward()        src/training/common.py:380-382
- *     -> ssip_conv_fwd / _dgrad / _wgrad, ssip_bn_*, ssip_maxpool_*,
- *        ssip_avgpool_fc_*                  (torchvision resnet18, :299-304)
+ *     -> ssip_conv_fwd / _dgrad / _dgrad_bn / _wgrad, ssip_bn_*,
+ *        ssip_stem_bn_pool_fwd / ssip_stem_pool_bn_bwd (bn1 -> relu -> maxpool),
+ *        ssip_maxpool_*, ssip_avgpool_fc_*   (torchvision resnet18, :299-304)
+ *     -> ssip_weight_prep_batch            (the conv weights each forward reads)
  *   criterion(outputs, labels)             src/training/common.py:381
  *     -> ssip_cross_entropy                (nn.CrossEntropyLoss, semi_supervised.py:111)
  *   optimizer.step()                       src/training/common.py:383
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 1
+#define SSIP_ABI_VERSION 2
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };

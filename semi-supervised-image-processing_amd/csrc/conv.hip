@@ -83,6 +83,7 @@ struct ConvArgs {
   // r = r0 + 2*ri, s = s0 + 2*si reach them, at dy row p = i + bh - ri.
   int phased;
   PhaseInfo phase[4];
+  int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
 };
 
 template <typename T> struct Traits;
@@ -354,7 +355,7 @@ struct RowMap {
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
                                                    int n0, int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
-                                                   bool pre_loaded, const RowMap& rmap) {
+                                                   bool pre_loaded, const RowMap& rmap, int split) {
   constexpr int NT = 64 * WMW * WNW;
   constexpr int WTM = BM / WMW, WTN = BN / WNW;
   const int tid = threadIdx.x;
@@ -363,7 +364,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
   const int rbase = wm * WTM + (lane >> 4) * 4;
   const int cbase = wn * WTN + (lane & 15);
   if constexpr (MODE == MODE_WGRAD) {
-    float* slab = static_cast<float*>(a.out) + (long)blockIdx.y * a.M * a.Ng;
+    float* slab = static_cast<float*>(a.out) + (long)split * a.M * a.Ng;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -517,14 +518,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM
   RowMap rmap;
   rmap.M = a.M;
   rmap.phased = false;
-  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false, rmap);
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false, rmap,
+                                                        (int)blockIdx.y);
 }
 
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0, int n0,
                                               int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
-                                              const RowMap& rmap) {
-  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, pre, true, rmap);
+                                              const RowMap& rmap, int split) {
+  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, pre, true, rmap, split);
 }
 
 // ---------------------------------------------------------------------------
@@ -851,8 +853,21 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
-  const int tn = blockIdx.x % a.tiles_n;
-  const int tm = blockIdx.x / a.tiles_n;
+  // XCD-aware order: the hardware deals workgroups round-robin to the 8 XCDs
+  // (each with its own L2); remap so every XCD owns a contiguous run of
+  // tiles (same split/phase, neighbouring M-tiles sharing im2col rows and the
+  // whole weight panel) instead of every 8th tile.
+  int bx, by;
+  {
+    const int nb = gridDim.x * gridDim.y;
+    const int lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const int xcd = lin & 7, q = nb >> 3, r = nb & 7;
+    const int t = a.xcd_remap ? xcd * q + min(xcd, r) + (lin >> 3) : lin;
+    bx = t % gridDim.x;
+    by = t / gridDim.x;
+  }
+  const int tn = bx % a.tiles_n;
+  const int tm = bx / a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const T* __restrict__ Ag = static_cast<const T*>(a.A);
   const T* __restrict__ Bg = static_cast<const T*>(a.B);
@@ -861,7 +876,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   // (field-wise constant-index selects: a dynamic index into the kernel
   // argument struct, or a pointer into a copy, lands it in scratch)
   const bool phased = (MODE == MODE_DGRAD) && a.phased;
-  const int f = phased ? (int)blockIdx.y : 0;
+  const int f = phased ? by : 0;
 #define SSIP_PSEL(fld) \
   (f == 0 ? a.phase[0].fld : f == 1 ? a.phase[1].fld : f == 2 ? a.phase[2].fld : a.phase[3].fld)
   RowMap rmap;
@@ -950,7 +965,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       b_ptr[t] = Bg + (long)(b_ok[t] ? n : 0) * a.Kg + c * 8;
     }
   } else {
-    mstart = (long)blockIdx.y * a.ksteps * BK;
+    mstart = (long)by * a.ksteps * BK;
     mend = mstart + (long)a.ksteps * BK;
     if (mend > a.Mred) mend = a.Mred;
     constexpr int CPA = BM / 8, RPA = 64 / CPA;
@@ -1113,7 +1128,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();
-  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap);
+  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -1297,6 +1312,10 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   a.tiles_n = ceil_div(a.Ng, pl.bn);
   const int tiles_m = ceil_div(a.M, pl.bm);
   pl.grid = dim3(tiles_m * a.tiles_n, pl.splits, 1);
+  {
+    const char* e = getenv("SSIP_CONV_NO_XCD");
+    a.xcd_remap = (e && e[0] == '1') ? 0 : 1;
+  }
   return SSIP_OK;
 }
 

@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-weak", action="store_true", help="run the weak forward on the main stream (A/B)")
+    ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50"],
+                    help="resnet50 + --image-size 512 --batch 128 = BASELINE config 5 (per GPU)")
+    ap.add_argument("--image-size", type=int, default=224)
     return ap.parse_args()
 
 
@@ -63,7 +66,7 @@ def main():
     Bl = args.labeled
     Bu = args.batch - Bl
     torch.manual_seed(42)
-    model = replace_fc(SSIPResNet("resnet18", 1000, dtype=args.dtype), 2).to(dev).train()
+    model = replace_fc(SSIPResNet(args.arch, 1000, dtype=args.dtype), 2).to(dev).train()
     if world > 1:
         # identical initial weights on every rank (rank 0 broadcasts)
         arena = model.flatten_parameters()
@@ -71,12 +74,13 @@ def main():
         for b in model.buffers():
             dist.broadcast(b, 0)
     bucketer = GradBucketer(model.flatten_parameters()) if world > 1 else None
-    step = SemiStep(model, lr=1e-4, weight_decay=1e-4, tau=0.7, bucketer=bucketer, seed=rank)
+    S = args.image_size
+    step = SemiStep(model, lr=1e-4, weight_decay=1e-4, tau=0.7, image_size=S, bucketer=bucketer, seed=rank)
     step.overlap = not args.serial_weak
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-    x_l = torch.randint(0, 256, (Bl, 224, 224, 3), generator=g, dtype=torch.uint8).to(dev)
-    x_u = torch.randint(0, 256, (Bu, 224, 224, 3), generator=g, dtype=torch.uint8).to(dev)
+    x_l = torch.randint(0, 256, (Bl, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    x_u = torch.randint(0, 256, (Bu, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
     y_l = torch.randint(0, 2, (Bl,), generator=g).to(dev)
 
     for _ in range(args.warmup):
@@ -132,7 +136,9 @@ def main():
         imgs = args.batch * world * args.steps
         value = imgs / elapsed
         res = {
-            "metric": "images/sec semi-supervised train step, 224x224 bs=256, 1/2/4/8 MI355X",
+            "metric": "images/sec semi-supervised train step, 224x224 bs=256, 1/2/4/8 MI355X"
+                      if (args.arch, S, args.batch) == ("resnet18", 224, 256) else
+                      f"images/sec semi-supervised train step, {args.arch} {S}x{S} bs={args.batch}",
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -143,13 +149,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic uint8 224x224x3 images resident in HBM, random-init ResNet-18 (seed 42)",
-            "config": {"workload": "semi_consistency_resnet18_224",
-                       "model": "resnet18", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                       "labeled_per_gpu": Bl, "unlabeled_per_gpu": Bu, "image_size": 224,
+            "data": f"synthetic uint8 {S}x{S}x3 images resident in HBM, random-init {args.arch} (seed 42)",
+            "config": {"workload": f"semi_consistency_{args.arch}_{S}",
+                       "model": args.arch, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "labeled_per_gpu": Bl, "unlabeled_per_gpu": Bu, "image_size": S,
                        "parallelism": f"dp{world}", "tau": 0.7,
                        "gflop_per_step_per_gpu": round(Bl * GFLOP_PER_IMG_TRAIN + Bu * (GFLOP_PER_IMG_FWD
-                                                                                        + GFLOP_PER_IMG_TRAIN), 1)},
+                                                                                        + GFLOP_PER_IMG_TRAIN), 1)
+                       if (args.arch, S) == ("resnet18", 224) else round(conv_flops / 1e9, 1)},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_note": "bytes per step for the same conv family, PMC FETCH_SIZE*2 + WRITE_SIZE "

@@ -1106,25 +1106,29 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
     const char* As = smem + stage * STAGE;
     const char* Bs = As + A_BYTES;
+    // both k-halves' fragments are requested before the first MFMA, so the
+    // second half's LDS reads overlap the first half's matrix work
+    Frag<T> fa[2][FM], fb[2][FN];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      Frag<T> fa[FM], fb[FN];
       if constexpr (!WG) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) read_kfrag(fa[i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
+        for (int i = 0; i < FM; ++i) read_kfrag(fa[h][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) read_kfrag(fb[j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, h);
+        for (int j = 0; j < FN; ++j) read_kfrag(fb[h][j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, h);
       } else {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[i], As, wm * WTM + i * 16, lane, h);
+        for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[h][i], As, wm * WTM + i * 16, lane, h);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[j], Bs, wn * WTN + j * 16, lane, h);
+        for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[h][j], Bs, wn * WTN + j * 16, lane, h);
       }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
-    }
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();

@@ -1328,12 +1328,12 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(256, 128, 4, 2, 3) X(256, 128, 4, 2, 2) X(256, 64, 4, 1, 2) X(256, 64, 4, 1, 3) X(256, 64, 4, 2, 2)        \
   X(256, 64, 4, 2, 3) X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 2, 3)      \
   X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
-  X(256, 128, 4, 4, 2)
+  X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)
 #define SSIP_GLDS_WG(X)                                                                                      \
   X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
   X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
   X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
-  X(64, 128, 1, 8, 2)
+  X(64, 128, 1, 8, 2) X(128, 128, 4, 4, 3) X(64, 128, 2, 4, 3) X(128, 64, 2, 4, 3) X(256, 128, 4, 4, 2)
 
 #define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
 

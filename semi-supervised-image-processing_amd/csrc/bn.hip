@@ -105,22 +105,23 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* be
 
 // z = act(y*scale + shift (+ residual)), 8 channels per thread.  The grid
 // stride is a multiple of C/8 (blockDim 256, C/8 | 256), so each thread keeps
-// one channel chunk and its scale/shift in registers.
+// one channel chunk and its scale/shift in registers; the grid is sized so a
+// thread handles several vectors (the per-channel loads are amortised), two
+// of them in flight per iteration.
 template <typename T>
-__global__ void bn_apply_kernel(int total8, int C, const T* __restrict__ y, const float* __restrict__ scale,
-                                const float* __restrict__ shift, const T* __restrict__ res, int relu,
-                                T* __restrict__ z) {
+__global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const T* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const T* __restrict__ res,
+                                                       int relu, T* __restrict__ z) {
   const int cpr = C >> 3;
   const int start = blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (start % cpr) * 8;
   float sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  load_f8(sc, scale + c0);
+  load_f8(sh, shift + c0);
   const int stride = gridDim.x * blockDim.x;
-  for (int i = start; i < total8; i += stride) {
-    Vec8<T> v, r, o;
-    v.load(y + (long)i * 8);
-    if (res) r.load(res + (long)i * 8);
+  auto one = [&](const Vec8<T>& v, const Vec8<T>& r, int i) {
+    Vec8<T> o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = __builtin_fmaf(v.get(j), sc[j], sh[j]);  // the stem's fused kernels repeat this exactly
@@ -129,6 +130,24 @@ __global__ void bn_apply_kernel(int total8, int C, const T* __restrict__ y, cons
       o.set(j, t);
     }
     o.store(z + (long)i * 8);
+  };
+  int i = start;
+  for (; i + stride < total8; i += 2 * stride) {
+    Vec8<T> v0, v1, r0, r1;
+    v0.load(y + (long)i * 8);
+    v1.load(y + (long)(i + stride) * 8);
+    if (res) {
+      r0.load(res + (long)i * 8);
+      r1.load(res + (long)(i + stride) * 8);
+    }
+    one(v0, r0, i);
+    one(v1, r1, i + stride);
+  }
+  if (i < total8) {
+    Vec8<T> v0, r0;
+    v0.load(y + (long)i * 8);
+    if (res) r0.load(res + (long)i * 8);
+    one(v0, r0, i);
   }
 }
 
@@ -151,10 +170,12 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
   float sd[8], sx[8], mu[8], is[8], msc[8], msh[8];
   const bool amask = mscale != nullptr;  // ReLU mask recomputed from y (no z read)
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sd[j] = 0.f; sx[j] = 0.f; mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j];
-    msc[j] = amask ? mscale[c0 + j] : 0.f;
-    msh[j] = amask ? mshift[c0 + j] : 0.f;
+  for (int j = 0; j < 8; ++j) { sd[j] = 0.f; sx[j] = 0.f; msc[j] = 0.f; msh[j] = 0.f; }
+  load_f8(mu, mean + c0);
+  load_f8(is, invstd + c0);
+  if (amask) {
+    load_f8(msc, mscale + c0);
+    load_f8(msh, mshift + c0);
   }
   if (rsub < rpi) {
     for (long r = r0 + rsub; r < r1; r += rpi) {
@@ -197,27 +218,26 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
 }
 
 template <typename T>
-__global__ void bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz, const T* __restrict__ zmask,
-                                    const T* __restrict__ y, const float* __restrict__ coef, T* __restrict__ dy,
-                                    T* __restrict__ dpre, const float* __restrict__ mscale,
-                                    const float* __restrict__ mshift) {
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz,
+                                                           const T* __restrict__ zmask, const T* __restrict__ y,
+                                                           const float* __restrict__ coef, T* __restrict__ dy,
+                                                           T* __restrict__ dpre, const float* __restrict__ mscale,
+                                                           const float* __restrict__ mshift) {
   const int cpr = C >> 3;
   const int start = blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (start % cpr) * 8;
   float ca[8], cb[8], cc[8], msc[8], msh[8];
   const bool amask = mscale != nullptr;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j];
-    msc[j] = amask ? mscale[c0 + j] : 0.f;
-    msh[j] = amask ? mshift[c0 + j] : 0.f;
+  load_f8(ca, coef + c0);
+  load_f8(cb, coef + C + c0);
+  load_f8(cc, coef + 2 * C + c0);
+  if (amask) {
+    load_f8(msc, mscale + c0);
+    load_f8(msh, mshift + c0);
   }
   const int stride = gridDim.x * blockDim.x;
-  for (int i = start; i < total8; i += stride) {
-    Vec8<T> g, zz, yy, o, p;
-    g.load(dz + (long)i * 8);
-    yy.load(y + (long)i * 8);
-    if (zmask) zz.load(zmask + (long)i * 8);
+  auto one = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& yy, int i) {
+    Vec8<T> o, p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float d = g.get(j);
@@ -228,6 +248,27 @@ __global__ void bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz,
     }
     o.store(dy + (long)i * 8);
     if (dpre) p.store(dpre + (long)i * 8);
+  };
+  int i = start;
+  for (; i + stride < total8; i += 2 * stride) {
+    Vec8<T> g0, g1, z0, z1, y0, y1;
+    g0.load(dz + (long)i * 8);
+    g1.load(dz + (long)(i + stride) * 8);
+    y0.load(y + (long)i * 8);
+    y1.load(y + (long)(i + stride) * 8);
+    if (zmask) {
+      z0.load(zmask + (long)i * 8);
+      z1.load(zmask + (long)(i + stride) * 8);
+    }
+    one(g0, z0, y0, i);
+    one(g1, z1, y1, i + stride);
+  }
+  if (i < total8) {
+    Vec8<T> g0, z0, y0;
+    g0.load(dz + (long)i * 8);
+    y0.load(y + (long)i * 8);
+    if (zmask) z0.load(zmask + (long)i * 8);
+    one(g0, z0, y0, i);
   }
 }
 
@@ -251,10 +292,20 @@ static int grid_for(long n, int per_block = 256) {
   return (int)b;
 }
 
+// elementwise BN passes: >= 4 vectors per thread where the tensor allows,
+// at most 2048 workgroups (8 per CU)
+static int bn_elem_grid(long total8) {
+  long b = (total8 + 1023) / 1024;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
 static int bwd_rows_per_block(long M, int C) {
-  // aim for ~1024 blocks, at least one full iteration of rows
+  // aim for ~512 blocks, at least four full iterations of rows
   const int rpi = 256 / (C / 8);
-  long rows = (M + 1023) / 1024;
+  long rows = (M + 511) / 512;
+  if (rows < 4 * rpi) rows = 4 * rpi;
   if (rows < rpi) rows = rpi;
   rows = ((rows + rpi - 1) / rpi) * rpi;
   return (int)rows;
@@ -292,7 +343,7 @@ int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply: unsupported size");
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, (hipStream_t)stream, total8, C,
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream, total8, C,
                        (const T*)y, scale, shift, (const T*)residual, relu, (T*)z);
   });
   return ::ssip::check_launch("bn_apply");
@@ -320,7 +371,7 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
                        (const T*)zmask, (const T*)y, mean, invstd, mscale, mshift, partial);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, blocks, (long)M, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
                        (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
@@ -338,7 +389,7 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, tiles, (long)M, partial, gamma, mean,
                      invstd, dgamma, dbeta, accumulate, coef);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
                        (const T*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr, (const float*)nullptr,
                        (const float*)nullptr);
   });

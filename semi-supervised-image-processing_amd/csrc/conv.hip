@@ -303,7 +303,7 @@ __device__ __forceinline__ void dgrad_bn_post(const ConvArgs& a, char* smem, int
   }
   // lanes l, l+CPR, ... of a wave share a chunk: butterfly over the lane
   // bits above log2(CPR), then combine the waves in fixed order via LDS.
-  static_assert(CPR == 8 || CPR == 16, "chunk count per row");
+  static_assert(CPR == 8 || CPR == 16 || CPR == 32, "chunk count per row");
 #pragma unroll
   for (int o = CPR; o < 64; o <<= 1) {
 #pragma unroll
@@ -352,7 +352,7 @@ struct RowMap {
   }
 };
 
-template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
+template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN, bool ALLOW_POST = true>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
                                                    int n0, int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
                                                    bool pre_loaded, const RowMap& rmap, int split) {
@@ -395,7 +395,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
         }
   }
   __syncthreads();
-  if constexpr (MODE == MODE_DGRAD) {
+  if constexpr (MODE == MODE_DGRAD && ALLOW_POST) {
     if (a.pmask != nullptr) {
       if (pre_loaded) {
         dgrad_bn_post<T, BM, BN, NT>(a, smem, m0, n0, tm, pre);
@@ -828,7 +828,9 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 // C4: the stem conv on a pre-padded 4-channel image (pad 0, S padded to 8,
 // even W): a 16-B chunk is a pixel pair (s, s+1) of one filter row, so a
 // 64-deep k-step covers filter rows 2ks and 2ks+1; k >= R*S*4 reads zeros.
-template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false>
+// POST: DGRAD with the BN-backward epilogue (ssip_conv_dgrad_bn); its
+// operand registers are only allocated in that instantiation.
+template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false>
 __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
     conv_glds_kernel(const ConvArgs a) {
   typedef __bf16 T;
@@ -1095,9 +1097,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   // step ks-1.
   // fused-BN epilogue operands: issued first, landed long before the epilogue
   BnPostRegs<T, BM, BN, 64 * WMW * WNW> post;
-  if constexpr (MODE == MODE_DGRAD) {
-    if (a.pmask != nullptr) post.load(a, m0, n0);
-  }
+  if constexpr (MODE == MODE_DGRAD && POST) post.load(a, m0, n0);
   if (nsteps > 0) issue(0, 0);
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
@@ -1108,9 +1108,12 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     const char* Bs = As + A_BYTES;
     // both k-halves' fragments are requested before the first MFMA, so the
     // second half's LDS reads overlap the first half's matrix work
+    // (wave tiles of more than 8 fragments read one k-half at a time)
+    constexpr bool BOTH = FM + FN <= 8;
     Frag<T> fa[2][FM], fb[2][FN];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      if (!BOTH && h == 1) break;
       if constexpr (!WG) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) read_kfrag(fa[h][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
@@ -1124,15 +1127,32 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h) {
+      if (!BOTH && h == 1) {
+        if constexpr (!WG) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) read_kfrag(fa[1][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, 1);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) read_kfrag(fb[1][j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, 1);
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[1][i], As, wm * WTM + i * 16, lane, 1);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[1][j], Bs, wn * WTN + j * 16, lane, 1);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
+    }
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();
-  conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
+  if constexpr (MODE == MODE_DGRAD && POST)
+    conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
+  else
+    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN, false>(a, acc, smem, m0, n0, tm, post, false, rmap, by);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -1328,13 +1348,16 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(256, 128, 4, 2, 3) X(256, 128, 4, 2, 2) X(256, 64, 4, 1, 2) X(256, 64, 4, 1, 3) X(256, 64, 4, 2, 2)        \
   X(256, 64, 4, 2, 3) X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 2, 3)      \
   X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
-  X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)
+  X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)             \
+  X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2)
 #define SSIP_GLDS_WG(X)                                                                                      \
   X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
   X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
   X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
-  X(64, 128, 1, 8, 2) X(128, 128, 4, 4, 3) X(64, 128, 2, 4, 3) X(128, 64, 2, 4, 3) X(256, 128, 4, 4, 2)
+  X(64, 128, 1, 8, 2) X(128, 128, 4, 4, 3) X(64, 128, 2, 4, 3) X(128, 64, 2, 4, 3) X(256, 128, 4, 4, 2)    \
+  X(128, 256, 2, 2, 2) X(256, 128, 2, 2, 2) X(64, 256, 1, 2, 2) X(256, 256, 2, 2, 2)
 
+#define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
 #define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st) {
@@ -1362,6 +1385,20 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
   if constexpr (MODE == MODE_WGRAD) {
     SSIP_GLDS_WG(SSIP_GLDS_GO)
   } else {
+    if constexpr (MODE == MODE_DGRAD) {
+      if (pl.args.pmask != nullptr) {  // fused BN-backward epilogue: default tiles only
+#define SSIP_GLDS_GOP(BM_, BN_, WM_, WN_, ST_)                                                                \
+  if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, true>), pl.grid,               \
+                       dim3(64 * WM_ * WN_), 0, st, pl.args);                                                 \
+    return ::ssip::check_launch("conv_glds_bnpost");                                                          \
+  }
+        SSIP_GLDS_POST(SSIP_GLDS_GOP)
+#undef SSIP_GLDS_GOP
+        ::ssip::set_error("no fused-BN dgrad kernel for %dx%d/%dx%d/%d", pl.bm, pl.bn, pl.wmw, pl.wnw, pl.stages);
+        return SSIP_ERR_ARG;
+      }
+    }
     if constexpr (MODE == MODE_FWD) {
       if (pl.conv1) {
 #define SSIP_GLDS_GO4(BM_, BN_, WM_, WN_, ST_)                                                                \
@@ -1531,6 +1568,12 @@ int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const
   if (rc) return rc;
   SSIP_REQUIRE(dy && w_crsk && zmask && y && mean && invstd && dpre && partial, SSIP_ERR_ARG,
                "ssip_conv_dgrad_bn: null pointer");
+  if (pl.stages > 0 && !getenv("SSIP_CONV_FORCE")) {  // the fused epilogue is built for the 128-row tiles only
+    pl.bm = 128; pl.wmw = 4; pl.wnw = 2; pl.stages = 2;
+    pl.bn = (pl.args.Ng % 128 == 0) ? 128 : 64;
+    pl.args.tiles_n = ceil_div(pl.args.Ng, pl.bn);
+    pl.grid = dim3(ceil_div(pl.args.M, pl.bm) * pl.args.tiles_n, 1, 1);
+  }
   SSIP_REQUIRE(pl.bm >= 128, SSIP_ERR_ARG, "ssip_conv_dgrad_bn: partial sizing assumes >= 128-row tiles");
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dpre; pl.args.add = dx_add;
   pl.args.pmask = zmask; pl.args.py = y; pl.args.pmean = mean; pl.args.pinvstd = invstd; pl.args.partial = partial;

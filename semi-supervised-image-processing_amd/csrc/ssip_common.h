@@ -80,6 +80,15 @@ template <> struct Vec8<float> {
   }
 };
 
+// 8 consecutive floats (32-B aligned: channel chunks of 8) as two 16-B loads
+__device__ __forceinline__ void load_f8(float (&d)[8], const float* p) {
+  typedef __attribute__((ext_vector_type(4))) float f4;
+  const f4 a = reinterpret_cast<const f4*>(p)[0];
+  const f4 b = reinterpret_cast<const f4*>(p)[1];
+  d[0] = a[0]; d[1] = a[1]; d[2] = a[2]; d[3] = a[3];
+  d[4] = b[0]; d[5] = b[1]; d[6] = b[2]; d[7] = b[3];
+}
+
 // ---------------------------------------------------------------------------
 // wave reductions (wave64)
 // ---------------------------------------------------------------------------

@@ -36,8 +36,8 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
   const int n = row / P, p = row - (row / P) * P;
   const int cc = threadIdx.x % cpr;
   float sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = scale[cc * 8 + j]; sh[j] = shift[cc * 8 + j]; }
+  load_f8(sc, scale + cc * 8);
+  load_f8(sh, shift + cc * 8);
   const T* yb = y + (long)n * H * W * C + cc * 8;
   for (int e = threadIdx.x; e < Q * cpr; e += blockDim.x) {
     const int q = e / cpr;
@@ -151,11 +151,11 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_reduce_kernel(
   const int c0 = chunk * 8;
   float sd[8], sx[8], mu[8], is[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sd[j] = 0.f; sx[j] = 0.f;
-    mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j];
-    sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j];
-  }
+  for (int j = 0; j < 8; ++j) { sd[j] = 0.f; sx[j] = 0.f; }
+  load_f8(mu, mean + c0);
+  load_f8(is, invstd + c0);
+  load_f8(sc, scale + c0);
+  load_f8(sh, shift + c0);
   const int row0 = blockIdx.x * rows;
   const int row1 = min(row0 + rows, N * H);
   for (int row = row0; row < row1; ++row) {
@@ -216,11 +216,11 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_apply_kernel(
   const int cc = threadIdx.x % cpr;
   const int c0 = cc * 8;
   float ca[8], cb[8], ck[8], sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; ck[j] = coef[2 * C + c0 + j];
-    sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j];
-  }
+  load_f8(ca, coef + c0);
+  load_f8(cb, coef + C + c0);
+  load_f8(ck, coef + 2 * C + c0);
+  load_f8(sc, scale + c0);
+  load_f8(sh, shift + c0);
   int plo, phi;
   pool_rows(h, P, k, s, pad, plo, phi);
   const T* dp = dpool + (long)n * P * Q * C + c0;

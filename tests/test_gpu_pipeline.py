@@ -91,7 +91,8 @@ def test_train_model_trajectory_matches_reference(dev, tmp_path):
     assert _rel(logits, gold["final_eval_logits"]) < 2e-2
     ref = np.asarray(gold["final_eval_logits"])
     margin = np.abs(ref[:, 1] - ref[:, 0])
-    safe = margin > 1e-2 * np.abs(ref).max()
+    # within the 2e-2 logit bound above, a margin under 2 x 2e-2 may flip
+    safe = margin > 4e-2 * np.abs(ref).max()
     assert (logits.argmax(1)[safe] == ref.argmax(1)[safe]).all()
 
 

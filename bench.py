@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50"],
                     help="resnet50 + --image-size 512 --batch 128 = BASELINE config 5 (per GPU)")
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python each step (default: replay one captured hipGraph)")
     return ap.parse_args()
 
 
@@ -75,7 +77,8 @@ def main():
             dist.broadcast(b, 0)
     bucketer = GradBucketer(model.flatten_parameters()) if world > 1 else None
     S = args.image_size
-    step = SemiStep(model, lr=1e-4, weight_decay=1e-4, tau=0.7, image_size=S, bucketer=bucketer, seed=rank)
+    step = SemiStep(model, lr=1e-4, weight_decay=1e-4, tau=0.7, image_size=S, bucketer=bucketer, seed=rank,
+                    graph=not args.eager)
     step.overlap = not args.serial_weak
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
@@ -105,7 +108,9 @@ def main():
     # roofline leg: one instrumented step, HIP events around every conv launch
     timer = ops.ConvTimer()
     ops.set_conv_timer(timer)
+    graph, step.graph = step.graph, False  # the same kernels launched one by one, each bracketed by events
     step(x_l, y_l, x_u)
+    step.graph = graph
     ops.set_conv_timer(None)
     summ = timer.summary()
     conv_flops = sum(v[0] for v in summ.values())

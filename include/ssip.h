@@ -200,6 +200,14 @@ int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, int out_pad
  * ---------------------------------------------------------------------- */
 int ssip_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, float grad_scale, void* stream);
+/* Graph-replayable AdamW (same update as ssip_adamw): the schedule lives on the
+ * device, sched = {lr, t, lr / (1 - beta1^t), sqrt(1 - beta2^t)} (fp64).
+ * ssip_adamw_sched_step advances t and the bias corrections (one thread);
+ * ssip_adamw_dev applies the update reading them, so no per-step host scalar
+ * is baked into a captured hipGraph.  (torch.optim.AdamW, semi_supervised.py:115-122) */
+int ssip_adamw_sched_step(double* sched, float beta1, float beta2, void* stream);
+int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const double* sched,
+                   float beta1, float beta2, float eps, float weight_decay, float grad_scale, void* stream);
 /* w_kcrs (fp32 torchvision layout) -> w_krsc [K][R][Sp][Cp] and/or w_crsk [Cp][R][Sp][K] in dtype */
 int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, const float* w_kcrs, void* w_krsc,
                      void* w_crsk, void* stream);

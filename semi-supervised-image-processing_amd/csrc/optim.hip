@@ -32,6 +32,39 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
   }
 }
 
+// Device-resident schedule (graph-replayable step): sched = {lr, t, lr/(1-b1^t),
+// sqrt(1-b2^t)} in fp64.  One thread advances t and the bias corrections
+// (the same double arithmetic the host path does); the update kernel reads
+// them, so a captured step needs no host-side scalars that change per step.
+__global__ void adamw_sched_kernel(double* sched, double b1, double b2) {
+  const double t = sched[1] + 1.0;
+  sched[1] = t;
+  sched[2] = sched[0] / (1.0 - pow(b1, t));
+  sched[3] = sqrt(1.0 - pow(b2, t));
+}
+
+__global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                 float* __restrict__ v, const double* __restrict__ sched, float b1, float b2,
+                                 float eps, float wd, float grad_scale) {
+  const float lr = (float)sched[0];
+  const float step_size = (float)sched[2];
+  const float bc2_sqrt = (float)sched[3];
+  const float decay = 1.f - lr * wd;
+  const float w1 = 1.f - b1;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * grad_scale;
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
 // w (KCRS, f32) -> out_krsc[K][R][Sp][Cp] and out_crsk[Cp][R][Sp][K] (zero padded)
 template <typename T>
 __global__ void weight_prep_kernel(int K, int C, int R, int S, int Cp, int Sp, const float* __restrict__ w,
@@ -116,6 +149,25 @@ int ssip_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float
   hipLaunchKernelGGL(adamw_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad, exp_avg,
                      exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, grad_scale);
   return ::ssip::check_launch("adamw");
+}
+
+int ssip_adamw_sched_step(double* sched, float beta1, float beta2, void* stream) {
+  SSIP_REQUIRE(sched, SSIP_ERR_ARG, "ssip_adamw_sched_step: null schedule");
+  hipLaunchKernelGGL(adamw_sched_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sched, (double)beta1,
+                     (double)beta2);
+  return ::ssip::check_launch("adamw_sched");
+}
+
+int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                   const double* sched, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+                   void* stream) {
+  SSIP_REQUIRE(n > 0 && param && grad && exp_avg && exp_avg_sq && sched, SSIP_ERR_ARG,
+               "ssip_adamw_dev: bad arguments");
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
+                     exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale);
+  return ::ssip::check_launch("adamw_dev");
 }
 
 int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, const float* w_kcrs, void* w_krsc,

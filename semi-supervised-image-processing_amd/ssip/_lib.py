@@ -96,6 +96,8 @@ _SIGS = {
     ),
     "ssip_nchw_to_nhwc": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp]),
     "ssip_adamw": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_f, _vp]),
+    "ssip_adamw_sched_step": (_c_int, [_vp, _c_f, _c_f, _vp]),
+    "ssip_adamw_dev": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _vp]),
     "ssip_weight_prep": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp, _vp]),
     "ssip_weight_prep_batch": (_c_int, [_c_int, _c_int, ctypes.POINTER(WPrep), _vp]),
 }

@@ -72,6 +72,13 @@ class GradBucketer:
             lo = min(spans[i][0] for i in idxs)
             hi = max(spans[i][0] + spans[i][1] for i in idxs)
             self.ranges.append((lo, hi))
+        # hipGraph mode (SemiStep(graph=True)): while the backward is being
+        # captured a completed bucket records an external event instead of
+        # launching; after each replay launch_after_graph() issues the
+        # all-reduces, each on the comm stream behind its bucket's event
+        self.capture_mode = False
+        self.events: List[Optional[torch.cuda.Event]] = [None] * len(buckets)
+        self._comm = None
         self.reset()
 
     def reset(self):
@@ -83,10 +90,38 @@ class GradBucketer:
         if self.launched[b]:
             return
         self.launched[b] = True
+        if self.capture_mode:
+            ev = torch.cuda.Event(external=True)
+            ev.record()
+            self.events[b] = ev
+            return
         lo, hi = self.ranges[b]
         if self.world > 1:
             self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                                 async_op=True))
+
+    def end_capture(self) -> None:
+        """Record the events of buckets still open at the end of the captured backward."""
+        for b in range(len(self.buckets)):
+            if any(self.params[i].requires_grad for i in self.buckets[b]):
+                self._launch(b)
+
+    def launch_after_graph(self) -> None:
+        """Issue every bucket's all-reduce behind the event its gradients'
+        last kernel records inside the replayed graph."""
+        if self._comm is None:
+            self._comm = torch.cuda.Stream()
+        self.handles = []
+        for b, ev in enumerate(self.events):
+            if ev is None:
+                continue
+            self._comm.wait_event(ev)
+            if self.world > 1:
+                lo, hi = self.ranges[b]
+                with torch.cuda.stream(self._comm):
+                    self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM,
+                                                        group=self.group, async_op=True))
+        self.launched = [True] * len(self.buckets)
 
     def mark_ready(self, params) -> None:
         idx = {id(p): i for i, p in enumerate(self.params)}
@@ -106,6 +141,8 @@ class GradBucketer:
         for h in self.handles:
             h.wait()
         self.handles = []
+        if self._comm is not None:  # graph mode: the comm stream also carried the event waits
+            torch.cuda.current_stream().wait_stream(self._comm)
         return 1.0 / self.world
 
 

@@ -355,6 +355,16 @@ def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
          float(beta2), float(eps), float(weight_decay), int(step), float(grad_scale), stream_ptr())
 
 
+def adamw_sched_step(sched: torch.Tensor, beta1: float, beta2: float) -> None:
+    assert sched.dtype == torch.float64 and sched.numel() == 4
+    call("ssip_adamw_sched_step", _p(sched), float(beta1), float(beta2), stream_ptr())
+
+
+def adamw_dev(param, grad, exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale=1.0) -> None:
+    call("ssip_adamw_dev", param.numel(), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(sched), float(beta1),
+         float(beta2), float(eps), float(weight_decay), float(grad_scale), stream_ptr())
+
+
 def nchw_to_nhwc(x: torch.Tensor, Cp: int, dtype: torch.dtype, pad: int = 0) -> torch.Tensor:
     """f32 NCHW -> [B, H+2*pad, W+2*pad, Cp] with a zero border and zero channel padding."""
     B, C, H, W = x.shape

@@ -27,6 +27,29 @@ class AdamW(torch.optim.Optimizer):
         self.arena = arena
         self._flat_state = None  # (exp_avg_flat, exp_avg_sq_flat) parallel to arena.flat
         self._runs_cache: Dict[int, List[Tuple[int, int, List[torch.Tensor]]]] = {}
+        self._sched = None     # per group: fp64 device tensor {lr, t, lr/(1-b1^t), sqrt(1-b2^t)}
+        self._sched_lr = None
+
+    def use_device_schedule(self) -> None:
+        """Keep lr and the step count on the device (``ssip_adamw_sched_step``
+        + ``ssip_adamw_dev``): ``step()`` then enqueues kernels only — no host
+        scalar changes per step, so it can run inside a captured hipGraph.
+        All parameters of a group advance together (torch keeps one count per
+        parameter; they agree whenever every parameter has a gradient)."""
+        if self._sched is not None:
+            return
+        self._ensure_flat_state()
+        dev = self.param_groups[0]["params"][0].device
+        self._sched, self._sched_lr = [], []
+        for group in self.param_groups:
+            t = 0.0
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    t = float(st["step"])
+                    break
+            self._sched.append(torch.tensor([group["lr"], t, 0.0, 0.0], dtype=torch.float64, device=dev))
+            self._sched_lr.append(group["lr"])
 
     def _ensure_flat_state(self):
         if self.arena is not None and self._flat_state is None:
@@ -66,6 +89,9 @@ class AdamW(torch.optim.Optimizer):
             if not params:
                 continue
             runs, loose = self._runs(gi, params)
+            if self._sched is not None:
+                self._step_device(gi, group, params, runs, loose, grad_scale)
+                continue
             # per-parameter state (views into the flat state for arena params)
             for p in params:
                 st = self.state[p]
@@ -92,3 +118,39 @@ class AdamW(torch.optim.Optimizer):
             # model's compute-dtype weight cache) that these tensors changed
             increment_version(params)
         return loss
+
+    def _init_state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0)
+            if self._flat_state is not None and self.arena.owns(p):
+                off, n = self.arena.span(p)
+                st["exp_avg"] = self._flat_state[0][off:off + n].view_as(p)
+                st["exp_avg_sq"] = self._flat_state[1][off:off + n].view_as(p)
+            else:
+                st["exp_avg"] = torch.zeros_like(p)
+                st["exp_avg_sq"] = torch.zeros_like(p)
+        return st
+
+    def _step_device(self, gi, group, params, runs, loose, grad_scale):
+        b1, b2 = group["betas"]
+        sched = self._sched[gi]
+        if group["lr"] != self._sched_lr[gi]:  # an LR scheduler moved it (host decision, eager only)
+            sched[0].fill_(group["lr"])
+            self._sched_lr[gi] = group["lr"]
+        for p in params:
+            self._init_state(p)
+        ops.adamw_sched_step(sched, b1, b2)
+        for off, n, ps in runs:
+            ops.adamw_dev(self.arena.flat[off:off + n], self.arena.grad[off:off + n],
+                          self._flat_state[0][off:off + n], self._flat_state[1][off:off + n], sched,
+                          b1, b2, group["eps"], group["weight_decay"], grad_scale)
+        for p in loose:
+            st = self.state[p]
+            ops.adamw_dev(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], sched, b1, b2,
+                          group["eps"], group["weight_decay"], grad_scale)
+        increment_version(params)
+
+    def device_step_count(self, gi: int = 0) -> int:
+        """The device-side step count (syncs)."""
+        return int(self._sched[gi][1].item()) if self._sched is not None else -1

@@ -241,10 +241,12 @@ class SSIPResNet(nn.Module):
             self._arena = ParamArena(list(self.parameters()))
         return self._arena
 
-    def prepare_weights(self, need_t: bool = True) -> None:
+    def prepare_weights(self, need_t: bool = True, force: bool = False) -> None:
         """Refresh the compute-dtype conv weight copies now (one launch) so a
-        later forward on another stream only reads them."""
-        _prepare_weights(self, need_t)
+        later forward on another stream only reads them.  force: refresh all
+        of them regardless of version (a captured step must always contain
+        the refresh)."""
+        _prepare_weights(self, need_t, force)
 
     # ------------------------------------------------------------------
     def forward(self, x):
@@ -310,7 +312,7 @@ def _geom(conv: nn.Conv2d, N: int, H: int, W: int, in_pad: int = 0) -> ConvGeom:
                     stride=conv.stride[0], pad=pad, c_real=C, s_real=S)
 
 
-def _prepare_weights(model: SSIPResNet, need_t: bool) -> None:
+def _prepare_weights(model: SSIPResNet, need_t: bool, force: bool = False) -> None:
     """Refresh the compute-dtype KRSC (forward) and CRSK (data-gradient)
     copies of every conv weight whose fp32 master changed since the last
     refresh (torch version counter; ssip.optim.AdamW bumps it), in one
@@ -323,7 +325,7 @@ def _prepare_weights(model: SSIPResNet, need_t: bool) -> None:
         w = conv.weight
         key = (id(conv), dt)
         ent = model._prep.get(key)
-        if ent is not None and ent[2] == w._version and (ent[1] is not None or not need_t):
+        if not force and ent is not None and ent[2] == w._version and (ent[1] is not None or not need_t):
             continue
         g = _geom(conv, 1, 1, 1)
         if ent is None or (need_t and ent[1] is None):

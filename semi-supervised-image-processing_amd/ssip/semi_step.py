@@ -38,8 +38,23 @@ class StepStats:
 
 
 class SemiStep:
+    """One call = one optimizer step.
+
+    graph=True: the first ``eager_warmup`` calls run eagerly; the next call
+    captures steps 1-5 (augment -> weak forward -> train forward -> loss ->
+    backward, ~260 kernel launches) into one hipGraph via torch.cuda.graph,
+    and every call from then on copies its inputs into the graph's static
+    buffers and replays it: no per-kernel host launch cost, no host gaps.
+    AdamW runs after the replay with its schedule on the device
+    (``AdamW.use_device_schedule``); with world > 1 the gradient buckets are
+    all-reduced between the replay and AdamW, each bucket waiting only on
+    the external event the graph records when its gradients are complete, so
+    RCCL still overlaps the rest of the backward.
+    """
+
     def __init__(self, model: SSIPResNet, lr: float = 1e-4, weight_decay: float = 1e-4, tau: float = 0.7,
-                 lambda_u: float = 1.0, image_size: int = 224, bucketer=None, seed: int = 0):
+                 lambda_u: float = 1.0, image_size: int = 224, bucketer=None, seed: int = 0, graph: bool = False,
+                 eager_warmup: int = 2):
         self.model = model
         self.arena = model.flatten_parameters()
         self.opt = AdamW(model.parameters(), lr=lr, weight_decay=weight_decay, arena=self.arena)
@@ -52,6 +67,12 @@ class SemiStep:
             model.grad_ready_hook = bucketer.mark_ready
         self.overlap = True   # weak forward on a second HIP stream
         self._side = None
+        self.graph = graph
+        self.eager_warmup = eager_warmup
+        self._calls = 0
+        self._g = None
+        if graph:
+            self.opt.use_device_schedule()
 
     def _side_stream(self, dev):
         if self._side is None:
@@ -65,48 +86,113 @@ class SemiStep:
                 draw_params_batch(Bu, s, False, self.gen).pin_memory(),
                 draw_params_batch(Bu, s, True, self.gen).pin_memory())
 
-    def __call__(self, x_l: torch.Tensor, y_l: torch.Tensor, x_u: torch.Tensor, params=None) -> StepStats:
-        """x_l [Bl,H,W,3] u8, y_l [Bl] int64, x_u [Bu,H,W,3] u8 — all on the device."""
+    # the three pieces of steps 1-5; each runs on the current stream and is
+    # capturable (no host sync, no host-side value that changes per step)
+    def _weak(self, x_u, pw) -> torch.Tensor:
+        """weak view + weak forward (batch-stat BN, no running update, no grad)."""
+        m = self.model
+        m.bn_update_running = False
+        with torch.no_grad():
+            zw = m(self.tf(x_u, pw))
+        m.bn_update_running = True
+        return zw
+
+    def _train_fwd(self, x_l, x_u, pl, ps) -> torch.Tensor:
+        """[labelled weak ; unlabelled strong] views and the joint train forward."""
         m = self.model
         Bl, Bu = x_l.shape[0], x_u.shape[0]
-        dev = x_l.device
-        if params is None:
-            params = self.draw_params(Bl, Bu)
-        pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
-        main = torch.cuda.current_stream(dev)
-        S = self.size
-        P = self.tf.pad
-        m.train()
-        # compute-dtype weights for both forwards, refreshed once, before the fork
-        m.prepare_weights(need_t=True)
-        # 2. weak view + weak forward on a side stream (batch-stat BN, no
-        #    running update, no grad): it only meets the train forward at the
-        #    loss, so the two latency-bound forwards overlap on the chip
-        side = self._side_stream(dev) if self.overlap else main
-        side.wait_stream(main)
-        m.bn_update_running = False
-        with torch.cuda.stream(side), torch.no_grad():
-            xw = self.tf(x_u, pw)
-            zw = m(xw)
-        m.bn_update_running = True
-        # 1+3. [labelled weak ; unlabelled strong] views and the joint train forward
-        x_ls = torch.empty((Bl + Bu, S + 2 * P, S + 2 * P, 4), device=dev, dtype=m.compute_dtype)
+        S, P = self.size, self.tf.pad
+        x_ls = torch.empty((Bl + Bu, S + 2 * P, S + 2 * P, 4), device=x_l.device, dtype=m.compute_dtype)
         self.tf(x_l, pl, out=x_ls[:Bl])
         self.tf(x_u, ps, out=x_ls[Bl:])
         self.opt.zero_grad(set_to_none=True)
         if self.bucketer is not None:
             self.bucketer.reset()
-        logits = m(DeviceImages(x_ls, P))
+        return m(DeviceImages(x_ls, P))
+
+    def _loss_bwd(self, logits, y_l, zw) -> torch.Tensor:
+        """loss + dlogits in one launch, then the backward."""
+        Bl = y_l.shape[0]
+        out, dzl, dzs, pseudo, mask = ops.semi_loss(logits[:Bl].detach().contiguous(), y_l, zw.contiguous(),
+                                                    logits[Bl:].detach().contiguous(), self.tau, self.lambda_u)
+        logits.backward(torch.cat([dzl, dzs], 0))
+        return out
+
+    def _fwd_bwd(self, x_l, y_l, x_u, pl, pw, ps) -> torch.Tensor:
+        """Steps 1-5, eager: the weak forward on a side stream overlaps the
+        train forward (they only meet at the loss)."""
+        m = self.model
+        dev = x_l.device
+        main = torch.cuda.current_stream(dev)
+        m.train()
+        # compute-dtype weights for both forwards, refreshed once, before the fork
+        m.prepare_weights(need_t=True)
+        side = self._side_stream(dev) if self.overlap else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            zw = self._weak(x_u, pw)
+        logits = self._train_fwd(x_l, x_u, pl, ps)
         if side is not main:
             main.wait_stream(side)
             zw.record_stream(main)
-        # 4. loss + dlogits in one launch
-        out, dzl, dzs, pseudo, mask = ops.semi_loss(logits[:Bl].detach().contiguous(), y_l,
-                                                    zw.contiguous(), logits[Bl:].detach().contiguous(),
-                                                    self.tau, self.lambda_u)
-        # 5. backward
-        logits.backward(torch.cat([dzl, dzs], 0))
+        return self._loss_bwd(logits, y_l, zw)
+
+    def __call__(self, x_l: torch.Tensor, y_l: torch.Tensor, x_u: torch.Tensor, params=None) -> StepStats:
+        """x_l [Bl,H,W,3] u8, y_l [Bl] int64, x_u [Bu,H,W,3] u8 — all on the device."""
+        Bl, Bu = x_l.shape[0], x_u.shape[0]
+        dev = x_l.device
+        if params is None:
+            params = self.draw_params(Bl, Bu)
+        self._calls += 1
+        if self.graph and self._calls > self.eager_warmup:
+            return self._replay(x_l, y_l, x_u, params)
+        pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
+        out = self._fwd_bwd(x_l, y_l, x_u, pl, pw, ps)
         scale = self.bucketer.finish() if self.bucketer is not None else 1.0
         # 6. optimizer
         self.opt.step(grad_scale=scale)
         return StepStats(loss=out)
+
+    # ------------------------------------------------------------------
+    # hipGraph path
+    # ------------------------------------------------------------------
+    def _replay(self, x_l, y_l, x_u, params) -> StepStats:
+        if self._g is None:
+            self._capture(x_l, y_l, x_u, params)
+        else:
+            for dst, src in zip(self._static, (x_l, y_l, x_u) + tuple(params)):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src, non_blocking=True)
+        self._g.replay()
+        if self.bucketer is not None:
+            self.bucketer.launch_after_graph()
+            scale = self.bucketer.finish()
+        else:
+            scale = 1.0
+        self.opt.step(grad_scale=scale)
+        # the next replay reads the compute-dtype weights: refresh them now
+        self.model.prepare_weights(need_t=True, force=True)
+        return StepStats(loss=self._g_out)
+
+    def _capture(self, x_l, y_l, x_u, params):
+        """One graph for steps 1-5.  The weak and train forwards are captured
+        from two streams, but HIP executes graph nodes (and separately launched
+        graphs) one after another, so they run back to back; splitting the
+        step into per-stream graphs, or launching the weak forward eagerly
+        beside the replay, measured no faster on MI355X."""
+        dev = x_l.device
+        m = self.model
+        m.train()
+        self._static = (x_l.clone(), y_l.clone(), x_u.clone()) + tuple(p.to(dev) for p in params)
+        m.prepare_weights(need_t=True, force=True)
+        torch.cuda.synchronize(dev)
+        if self.bucketer is not None:
+            self.bucketer.capture_mode = True
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._g_out = self._fwd_bwd(*self._static)
+            if self.bucketer is not None:
+                self.bucketer.end_capture()
+        if self.bucketer is not None:
+            self.bucketer.capture_mode = False
+        self._g = g

@@ -806,6 +806,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW) conv_gemm_kernel(const ConvArg
 // ---------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) int g_zero16[4];
 
+
 __device__ __forceinline__ void glds16(const void* src, char* lds_block) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_block, 16, 0, 0);
@@ -888,6 +889,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   int ph_ns = a.S, ph_r0 = 0, ph_s0 = 0, ph_bh = 0, ph_bw = 0, ph_ksteps = a.ksteps;
   if (phased) {
     if (tm >= SSIP_PSEL(tiles_m)) return;
+    // a phase no tap reaches (1x1 stride-2 dgrad: 3 of 4) adds nothing: with
+    // the residual gradient accumulated in place there is nothing to write
+    if (!POST && SSIP_PSEL(ksteps) == 0 && a.add == a.out) return;
     rmap.M = SSIP_PSEL(M);
     rmap.ph = SSIP_PSEL(ph);
     rmap.pw = SSIP_PSEL(pw);
@@ -1157,38 +1161,55 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
 //   (accumulate ? dW : 0) + sum_split slab[split][k][(r*Sp + s)*Cp + c]
-// Block = 32 output elements x 8 split groups; each group sums a contiguous
-// split range in order, the 8 partials are combined in fixed order in LDS.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int Ng, int C, int R,
-                                    int S, int Cp, int Sp, float* __restrict__ dw, int accumulate) {
-  __shared__ float red[8][33];
-  const long total = (long)K * Ng;
-  const long sstride = (long)K * Ng;
-  const int el = threadIdx.x & 31, grp = threadIdx.x >> 5;
-  const long idx = (long)blockIdx.x * 32 + el;
-  const int per = (splits + 7) / 8;
+// A thread owns one 16-B vector (4 consecutive columns) in one of G split
+// groups (G a power of two, chosen so the grid has ~1024 workgroups); a
+// group sums its contiguous split range in order, then the G partials are
+// combined in fixed order through LDS: bitwise reproducible.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
+                                                           int Ng, int C, int R, int S, int Cp, int Sp,
+                                                           float* __restrict__ dw, int accumulate, int lg) {
+  typedef __attribute__((ext_vector_type(4))) float f4;
+  __shared__ f4 red[256];
+  const int G = 1 << lg, V = 256 >> lg;
+  const int v = threadIdx.x & (V - 1), grp = threadIdx.x >> (8 - lg);
+  const long total4 = (long)K * Ng / 4;
+  const long idx4 = (long)blockIdx.x * V + v;
+  const long sstride4 = total4;
+  const int per = (splits + G - 1) / G;
   const int s0 = grp * per;
   const int s1 = min(splits, s0 + per);
-  float acc = 0.f;
-  if (idx < total) {
-    const float* p = slab + idx;
-    for (int sp = s0; sp < s1; ++sp) acc += p[sp * sstride];
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (idx4 < total4) {
+    const f4* p = reinterpret_cast<const f4*>(slab) + idx4;
+    int sp = s0;
+    for (; sp + 4 <= s1; sp += 4) {
+      const f4 a0 = p[(long)sp * sstride4], a1 = p[(long)(sp + 1) * sstride4];
+      const f4 a2 = p[(long)(sp + 2) * sstride4], a3 = p[(long)(sp + 3) * sstride4];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; sp < s1; ++sp) acc += p[(long)sp * sstride4];
   }
-  red[grp][el] = acc;
+  red[threadIdx.x] = acc;
   __syncthreads();
-  if (grp == 0 && idx < total) {
-    float t = 0.f;
+  if (grp == 0 && idx4 < total4) {
+    f4 t = red[v];
+    for (int g = 1; g < G; ++g) t += red[g * V + v];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) t += red[g][el];
-    const int col = (int)(idx % Ng);
-    const int k = (int)(idx / Ng);
-    const int c = col % Cp;
-    const int rs = col / Cp;
-    const int s = rs % Sp;
-    const int r = rs / Sp;
-    if (c < C && s < S) {
-      const long o = (((long)k * C + c) * R + r) * S + s;
-      dw[o] = accumulate ? dw[o] + t : t;
+    for (int e = 0; e < 4; ++e) {
+      const long idx = idx4 * 4 + e;
+      const int col = (int)(idx % Ng);
+      const int k = (int)(idx / Ng);
+      const int c = col % Cp;
+      const int rs = col / Cp;
+      const int s = rs % Sp;
+      const int r = rs / Sp;
+      if (c < C && s < S) {
+        const long o = (((long)k * C + c) * R + r) * S + s;
+        dw[o] = accumulate ? dw[o] + t[e] : t[e];
+      }
     }
   }
 }
@@ -1349,7 +1370,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(256, 64, 4, 2, 3) X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 2, 3)      \
   X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
   X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)             \
-  X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2)
+  X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2) X(256, 256, 4, 2, 2) X(512, 64, 8, 1, 2)
 #define SSIP_GLDS_WG(X)                                                                                      \
   X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
   X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
@@ -1604,10 +1625,12 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, rc = launch_conv<MODE_WGRAD, T>(pl, st));
   if (rc) return rc;
-  const long total = (long)d->K * pl.args.Ng;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 31) / 32)), dim3(256), 0, st,
-                     (const float*)workspace, pl.splits, d->K, pl.args.Ng, c_real, d->R, s_real, d->C, d->S, dw_kcrs,
-                     accumulate);
+  const long total4 = (long)d->K * pl.args.Ng / 4;  // Ng = R*S*C: C % 32 == 0, or the stem's 7x8x4
+  int lg = 0;  // split groups: double while splits allow and the grid stays within ~1024 workgroups
+  while (lg < 6 && (2 << lg) <= pl.splits && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
+  const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
+                     pl.splits, d->K, pl.args.Ng, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
   return ::ssip::check_launch("wgrad_reduce");
 }
 

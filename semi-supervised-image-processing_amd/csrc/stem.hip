@@ -39,6 +39,47 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
   load_f8(sc, scale + cc * 8);
   load_f8(sh, shift + cc * 8);
   const T* yb = y + (long)n * H * W * C + cc * 8;
+  if (k == 3) {
+    // all nine window loads issued before the first compare (out-of-image
+    // taps are skipped by the ok mask, in the same r, u order)
+    for (int e = threadIdx.x; e < Q * cpr; e += blockDim.x) {
+      const int q = e / cpr;
+      Vec8<T> v[9];
+      bool ok[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int h = p * s - pad + r, w = q * s - pad + u;
+          ok[r * 3 + u] = h >= 0 && h < H && w >= 0 && w < W;
+          v[r * 3 + u].load(yb + (ok[r * 3 + u] ? (h * W + w) * C : 0));
+        }
+      float best[8];
+      int bi[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = -1; }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!ok[t]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = to_f32(from_f32<T>(bn_relu(v[t].get(j), sc[j], sh[j])));
+          if (bi[j] < 0 || f > best[j] || f != f) { best[j] = f; bi[j] = t; }
+        }
+      }
+      Vec8<T> o;
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o.set(j, best[j]);
+        packed |= (uint64_t)(uint8_t)bi[j] << (8 * j);
+      }
+      const long oi = ((long)row * Q + q) * C + cc * 8;
+      o.store(out + oi);
+      *reinterpret_cast<uint64_t*>(idx + oi) = packed;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < Q * cpr; e += blockDim.x) {
     const int q = e / cpr;
     float best[8];
@@ -243,9 +284,10 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_apply_kernel(
   }
 }
 
-// full-resolution rows (n, h) per reduction workgroup: ~2048 workgroups
+// full-resolution rows (n, h) per reduction workgroup: ~8192 workgroups
+// (each thread's gather chain is serial: parallelism comes from workgroups)
 static int rows_per_block(int N, int H) {
-  const int rows = (N * H + 2047) / 2048;
+  const int rows = (N * H + 8191) / 8192;
   return rows < 1 ? 1 : rows;
 }
 
@@ -283,9 +325,9 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   const long M = (long)N * H * W;
   SSIP_REQUIRE(M * C / 8 < (1l << 31), SSIP_ERR_ARG, "ssip_stem_pool_bn_bwd: too large");
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  hipStream_t st = (hipStream_t)stream;
   const int rows = rows_per_block(N, H);
   const int blocks = (N * H + rows - 1) / rows;
-  hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                        pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);

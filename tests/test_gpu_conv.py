@@ -180,3 +180,51 @@ def test_conv_dgrad_bn_fused(dev, shape, dtname, with_add):
     tol_s = 1e-4 if dt == torch.float32 else 2e-2
     assert _relerr(p[:, 0], sum_d) < tol_s
     assert _relerr(p[:, 1], sum_dx) < tol_s
+
+
+@pytest.mark.parametrize("shape", [(16, 64, 28, 28, 128, 3, 1, 1), (8, 128, 14, 14, 256, 1, 2, 0),
+                                   (4, 3, 64, 64, 64, 7, 2, 3, True)])
+def test_conv_wgrad_many_splits(dev, shape):
+    """bf16 wgrad with many split-K slabs (grouped vectorised slab reduction)
+    against the fp64 reference; three back-to-back launches give identical
+    bits (fixed summation order)."""
+    torch.manual_seed(4)
+    N, C, H, W, K, R, st, pd, pre = _unpack(shape)
+    dt = torch.bfloat16
+    g = _geom(*_unpack(shape))
+    x = torch.randn(N, C, H, W).bfloat16().float()
+    dy = torch.randn(N, K, g.P, g.Q).bfloat16().float()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, R, R), dy.double(), stride=st, padding=pd)
+    xh = _to_nhwc(x, g.C, dt, dev, pd if pre else 0)
+    dyh = _to_nhwc(dy, K, dt, dev)
+    ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
+    outs = []
+    for _ in range(3):
+        dw = torch.full((K, C, R, R), 7.0, device=dev)
+        ops.conv_wgrad(g, dyh, xh, dw, False, ws)
+        torch.cuda.synchronize()
+        outs.append(dw.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert _relerr(outs[0], ref) < 1e-4
+
+
+def test_conv_dgrad_in_place_add_skips_empty_phases(dev):
+    """1x1 stride-2 dgrad accumulated in place (dx_add is dx, as the engine
+    adds the downsample branch): 3 of 4 output phases receive no tap and are
+    left untouched; the result equals ref + the old dx."""
+    torch.manual_seed(5)
+    N, C, H, W, K, R, st, pd = 2, 128, 15, 15, 256, 1, 2, 0
+    dt = torch.bfloat16
+    g = _geom(N, C, H, W, K, R, st, pd)
+    w = (torch.randn(K, C, R, R) * 0.1).bfloat16().float()
+    dy = torch.randn(N, K, g.P, g.Q).bfloat16().float()
+    add = torch.randn(N, C, H, W).bfloat16().float()
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.double(), dy.double(), stride=st, padding=pd)
+    ref = (ref + add.double()).permute(0, 2, 3, 1)
+    crsk = torch.empty((C, R, R, K), device=dev, dtype=dt)
+    ops.weight_prep(w.to(dev), dt, C, R, None, crsk)
+    dyh = _to_nhwc(dy, K, dt, dev)
+    dx = _to_nhwc(add, C, dt, dev)
+    ops.conv_dgrad(g, dyh, crsk, dx, dx)
+    torch.cuda.synchronize()
+    assert _relerr(dx.cpu(), ref) < 1e-2

@@ -344,3 +344,4 @@ def test_bn_relu_bwd_affine_mask_matches_z_mask(dev, dtname):
     torch.cuda.synchronize()
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+

@@ -24,7 +24,7 @@ def main():
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, grid_y, workgroup_x, stream_id from kernels order by start").fetchall()
-    ends = [i for i, r in enumerate(rows) if "adamw" in r[0]]
+    ends = [i for i, r in enumerate(rows) if "adamw" in r[0] and "sched" not in r[0]]
     i0, i1 = ends[a.step - 1] + 1, ends[a.step] + 1
     step = rows[i0:i1]
     wall = (step[-1][2] - rows[i0 - 1][2]) / 1e3

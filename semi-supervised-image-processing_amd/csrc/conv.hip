@@ -84,6 +84,7 @@ struct ConvArgs {
   int phased;
   PhaseInfo phase[4];
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
+  uint32_t a_bytes, b_bytes;  // operand extents (LDS-DMA kernel buffer resources)
 };
 
 template <typename T> struct Traits;
@@ -812,6 +813,18 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_block) {
                                    (__attribute__((address_space(3))) void*)lds_block, 16, 0, 0);
 }
 
+// Buffer-resource LDS-DMA: a raw buffer over the whole operand, per-lane
+// 32-bit byte offsets.  An offset past the extent reads zeros (the padding /
+// out-of-tile taps), so a gather step costs a mask test and one add per lane
+// instead of 64-bit address arithmetic and a select against a zero page.
+constexpr uint32_t SSIP_OOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, char* lds_block) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_block, 16, voff, 0, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
@@ -832,7 +845,8 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 // POST: DGRAD with the BN-backward epilogue (ssip_conv_dgrad_bn); its
 // operand registers are only allocated in that instantiation.
 template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false>
-__global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
+__global__ void __launch_bounds__(64 * WMW * WNW,
+                                  NSTAGE == 5 ? 2 : glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
     conv_glds_kernel(const ConvArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, BK = 64;
@@ -842,14 +856,18 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   constexpr int A_BYTES = WG ? BK * BM * 2 : BM * 128;
   constexpr int B_BYTES = WG ? BK * BN * 2 : BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  static_assert(NSTAGE == 2 || NSTAGE == 3, "2 or 3 LDS stages");
+  // NSTAGE 5 = the ping-pong schedule on two LDS buffers (see the main loop)
+  static_assert(NSTAGE == 2 || NSTAGE == 3 || NSTAGE == 5, "2 or 3 LDS stages, or ping-pong");
+  constexpr bool PP = NSTAGE == 5;
+  constexpr int NBUF = PP ? 2 : NSTAGE;
+  static_assert(!PP || (NW == 8 && !POST), "ping-pong pairs the 8 waves of a workgroup two per SIMD");
   constexpr int IA = A_BYTES / 1024, IB = B_BYTES / 1024;
   constexpr int LA = IA / NW, LB = IB / NW;
   constexpr int L = LA + LB;
   static_assert(IA % NW == 0 && IB % NW == 0 && LA >= 1 && LB >= 1, "bad glds tile");
   static_assert(FM >= 1 && FN >= 1, "bad wave tile");
   constexpr int EPI = WG ? 0 : BM * (BN * 2 + 16);
-  constexpr int SMEM = (NSTAGE * STAGE > EPI) ? NSTAGE * STAGE : EPI;
+  constexpr int SMEM = (NBUF * STAGE > EPI) ? NBUF * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
@@ -886,7 +904,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   rmap.phased = phased;
   rmap.H = a.H;
   rmap.W = a.W;
-  int ph_ns = a.S, ph_r0 = 0, ph_s0 = 0, ph_bh = 0, ph_bw = 0, ph_ksteps = a.ksteps;
+  int ph_nr = a.R, ph_ns = a.S, ph_r0 = 0, ph_s0 = 0, ph_bh = 0, ph_bw = 0, ph_ksteps = a.ksteps;
   if (phased) {
     if (tm >= SSIP_PSEL(tiles_m)) return;
     // a phase no tap reaches (1x1 stride-2 dgrad: 3 of 4) adds nothing: with
@@ -902,6 +920,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     rmap.div_w.d = SSIP_PSEL(div_w.d);
     rmap.div_w.mul = SSIP_PSEL(div_w.mul);
     rmap.div_w.shr = SSIP_PSEL(div_w.shr);
+    ph_nr = SSIP_PSEL(nr);
     ph_ns = SSIP_PSEL(ns);
     ph_r0 = SSIP_PSEL(r0);
     ph_s0 = SSIP_PSEL(s0);
@@ -999,6 +1018,45 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     }
   }
 
+  // buffer-resource state (FWD except the stem, DGRAD stride 1 / phase-split,
+  // WGRAD's dY operand): byte offset of the lane's chunk at tap 0 and the
+  // taps (bit r*S + s) whose source pixel lies inside the image.
+  constexpr bool BUF_A = !C4;
+  uint32_t a_off[LA], a_msk[LA], b_off[LB];
+  __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ag, a.a_bytes), rsB = make_rsrc(Bg, a.b_bytes);
+  if constexpr (!WG && BUF_A) {
+    const int nr = phased ? ph_nr : a.R, ns = phased ? ph_ns : a.S;
+#pragma unroll
+    for (int t = 0; t < LA; ++t) {
+      // valid taps: rows [lr, hr) x columns [ls, hs) of the (nr x ns) filter
+      int lr, hr, ls, hs;
+      long pix;
+      if constexpr (MODE == MODE_FWD) {  // input pixel (a_h + r, a_w + s)
+        lr = max(0, -a_h[t]); hr = min(nr, a.H - a_h[t]);
+        ls = max(0, -a_w[t]); hs = min(ns, a.W - a_w[t]);
+        pix = (long)a_base[t] + (long)a_h[t] * a.W + a_w[t];
+        a_off[t] = (uint32_t)((pix * a.C + a_c[t] * 8) * 2);
+      } else {  // dY pixel (a_h - r, a_w - s)
+        lr = max(0, a_h[t] - a.P + 1); hr = min(nr, a_h[t] + 1);
+        ls = max(0, a_w[t] - a.Q + 1); hs = min(ns, a_w[t] + 1);
+        pix = (long)a_base[t] + (long)a_h[t] * a.Q + a_w[t];
+        a_off[t] = (uint32_t)((pix * a.K + a_c[t] * 8) * 2);
+      }
+      const uint32_t cbits = hs > ls ? ((1u << hs) - 1u) & ~((1u << ls) - 1u) : 0u;
+      uint32_t msk = 0;
+      for (int r = 0; r < nr; ++r) msk |= (r >= lr && r < hr) ? cbits << (r * ns) : 0u;
+      a_msk[t] = a_ok[t] ? msk : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < LB; ++t) {
+      const int row = 8 * (wave + NW * t) + (lane >> 3);
+      b_off[t] = b_ok[t] ? (uint32_t)(((long)(n0 + row) * a.Kg + b_c[t] * 8) * 2) : 0xF0000000u;
+    }
+  } else if constexpr (WG) {
+#pragma unroll
+    for (int t = 0; t < LA; ++t) a_off[t] = (uint32_t)(((mstart + a_h[t]) * a.K + a_c[t]) * 2);
+  }
+
   auto issue = [&](int ks, int stage) {
     char* As = smem + stage * STAGE;
     char* Bs = As + A_BYTES;
@@ -1013,50 +1071,45 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
         glds16(src, As + (wave + NW * t) * 1024);
       }
     } else if constexpr (MODE == MODE_FWD) {
+      const int tp = kr * a.S + ks_;
+      const uint32_t toff = (uint32_t)(((kr * a.W + ks_) * a.C + kcb) * 2);
 #pragma unroll
       for (int t = 0; t < LA; ++t) {
-        const int hin = a_h[t] + kr, win = a_w[t] + ks_;
-        const bool ok = a_ok[t] && hin >= 0 && hin < a.H && win >= 0 && win < a.W;
-        const T* src = ok ? Ag + ((long)(a_base[t] + hin * a.W + win)) * a.C + kcb + a_c[t] * 8
-                          : reinterpret_cast<const T*>(g_zero16);
-        glds16(src, As + (wave + NW * t) * 1024);
+        const bool ok = (a_msk[t] >> tp) & 1u;
+        blds16(rsA, ok ? a_off[t] + toff : SSIP_OOB, As + (wave + NW * t) * 1024);
       }
     } else if constexpr (MODE == MODE_DGRAD) {
+      const int tp = kr * ph_ns + ks_;
+      const uint32_t toff = (uint32_t)((kcb - (kr * a.Q + ks_) * a.K) * 2);
 #pragma unroll
       for (int t = 0; t < LA; ++t) {
-        const int hp = a_h[t] - kr, wp = a_w[t] - ks_;
-        int p = hp, q = wp;
-        bool ok = a_ok[t] && hp >= 0 && wp >= 0;
-        if (!phased && a.stride != 1) {
-          ok = ok && ((hp | wp) & (a.stride - 1)) == 0;
-          p = hp >> (a.stride >> 1);
-          q = wp >> (a.stride >> 1);
-        }
-        ok = ok && p < a.P && q < a.Q;
-        const T* src = ok ? Ag + ((long)(a_base[t] + p * a.Q + q)) * a.K + kcb + a_c[t] * 8
-                          : reinterpret_cast<const T*>(g_zero16);
-        glds16(src, As + (wave + NW * t) * 1024);
+        const bool ok = (a_msk[t] >> tp) & 1u;
+        blds16(rsA, ok ? a_off[t] + toff : SSIP_OOB, As + (wave + NW * t) * 1024);
       }
     }
     if constexpr (!WG) {
 #pragma unroll
       for (int t = 0; t < LB; ++t) {
-        bool ok = b_ok[t];
-        if constexpr (C4) ok = ok && ks * BK + b_c[t] * 8 < a.Kg;
         int koff = ks * BK;
         if constexpr (MODE == MODE_DGRAD) {
           if (phased) koff = ((ph_r0 + 2 * kr) * a.S + ph_s0 + 2 * ks_) * a.K + kcb;
         }
-        const T* src = ok ? b_ptr[t] + koff : reinterpret_cast<const T*>(g_zero16);
-        glds16(src, Bs + (wave + NW * t) * 1024);
+        if constexpr (BUF_A) {
+          blds16(rsB, b_off[t] + (uint32_t)(koff * 2), Bs + (wave + NW * t) * 1024);
+        } else {
+          bool ok = b_ok[t];
+          if constexpr (C4) ok = ok && ks * BK + b_c[t] * 8 < a.Kg;
+          const T* src = ok ? b_ptr[t] + koff : reinterpret_cast<const T*>(g_zero16);
+          glds16(src, Bs + (wave + NW * t) * 1024);
+        }
       }
     } else {
+      const int mlim = (int)(mend - mstart) - ks * BK;  // rows of this k-step inside the split
+      const uint32_t moff = (uint32_t)(ks * BK * a.K * 2);
 #pragma unroll
       for (int t = 0; t < LA; ++t) {
-        const long m = mstart + (long)ks * BK + a_h[t];
-        const bool ok = a_ok[t] && m < mend;
-        const T* src = ok ? Ag + m * (long)a.K + a_c[t] : reinterpret_cast<const T*>(g_zero16);
-        glds16(src, As + (wave + NW * t) * 1024);
+        const bool ok = a_ok[t] && a_h[t] < mlim;
+        blds16(rsA, ok ? a_off[t] + moff : SSIP_OOB, As + (wave + NW * t) * 1024);
       }
 #pragma unroll
       for (int t = 0; t < LB; ++t) {
@@ -1102,6 +1155,77 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   // fused-BN epilogue operands: issued first, landed long before the epilogue
   BnPostRegs<T, BM, BN, 64 * WMW * WNW> post;
   if constexpr (MODE == MODE_DGRAD && POST) post.load(a, m0, n0);
+  if constexpr (PP) {
+    // Ping-pong (MI355X_MICROARCH.md "Two waves per SIMD"): waves 0-3
+    // (group 0) and 4-7 (group 1; one on each SIMD beside a group-0 wave)
+    // run the same k-steps one barrier interval apart, so in every interval
+    // one wave of each SIMD reads fragments while its partner runs MFMAs.
+    // Interval 2s: group 0 reads k-step s and issues its share of k-step s+1
+    // (into the buffer both groups finished reading before the interval);
+    // group 1 runs the MFMAs of s-1 and issues its share of s+1.
+    // Interval 2s+1: group 0 runs the MFMAs of s; group 1 reads s.  Every
+    // wave retires its own LDS-DMA with vmcnt(0) at the end of interval
+    // 2s+1, before the barrier after which k-step s+1 is first read.
+    const bool g1 = wave >= NW / 2;
+    Frag<T> fa[2][FM], fb[2][FN];
+    auto read_all = [&](int buf) {
+      const char* As = smem + buf * STAGE;
+      const char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (!WG) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) read_kfrag(fa[h][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) read_kfrag(fb[h][j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, h);
+        } else {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[h][i], As, wm * WTM + i * 16, lane, h);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[h][j], Bs, wn * WTN + j * 16, lane, h);
+        }
+      }
+    };
+    auto mfma_all = [&]() {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    if (nsteps > 0) {
+      issue(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (g1) {  // interval 0 of group 1: no MFMAs yet, only its share of k-step 1
+        if (nsteps > 1) issue(1, 1);
+        asm volatile("s_barrier" ::: "memory");
+      }
+      for (int ks = 0; ks < nsteps; ++ks) {
+        const int buf = ks & 1;
+        if (!g1) {
+          read_all(buf);
+          if (ks + 1 < nsteps) issue(ks + 1, buf ^ 1);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_all();
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+          read_all(buf);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_all();
+          if (ks + 2 < nsteps) issue(ks + 2, buf);
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_barrier" ::: "memory");
+        }
+      }
+      if (!g1) asm volatile("s_barrier" ::: "memory");
+    }
+  } else {
   if (nsteps > 0) issue(0, 0);
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
@@ -1152,6 +1276,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     }
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
+  }  // !PP
   __syncthreads();
   if constexpr (MODE == MODE_DGRAD && POST)
     conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
@@ -1270,6 +1395,11 @@ static void choose_glds(int mode, const ConvArgs& a, Plan& pl) {
   }
   pl.bm = 128; pl.wmw = 4; pl.wnw = 2;
   pl.bn = (a.Ng % 128 == 0) ? 128 : 64;
+  // 256x256 tiles (8 waves of 64x128) where a forward still has >= 160 of them
+  // (ResNet-18 layer3: 62.7 vs 69.1 us, profiles/r1_conv_tune.txt)
+  if (mode == MODE_FWD && a.Ng % 256 == 0 && (long)ceil_div(a.M, 256) * (a.Ng / 256) >= 160) {
+    pl.bm = 256; pl.bn = 256;
+  }
 }
 
 // Tuning override: SSIP_CONV_FORCE="<f|d|w>,bm,bn,waves_m,waves_n,stages"
@@ -1370,13 +1500,15 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(256, 64, 4, 2, 3) X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 2, 3)      \
   X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
   X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)             \
-  X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2) X(256, 256, 4, 2, 2) X(512, 64, 8, 1, 2)
+  X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2) X(256, 256, 4, 2, 2) X(512, 64, 8, 1, 2)      \
+  X(256, 128, 4, 2, 5) X(512, 64, 8, 1, 5) X(128, 128, 4, 2, 5) X(256, 64, 8, 1, 5)
 #define SSIP_GLDS_WG(X)                                                                                      \
   X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
   X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
   X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
   X(64, 128, 1, 8, 2) X(128, 128, 4, 4, 3) X(64, 128, 2, 4, 3) X(128, 64, 2, 4, 3) X(256, 128, 4, 4, 2)    \
-  X(128, 256, 2, 2, 2) X(256, 128, 2, 2, 2) X(64, 256, 1, 2, 2) X(256, 256, 2, 2, 2)
+  X(128, 256, 2, 2, 2) X(256, 128, 2, 2, 2) X(64, 256, 1, 2, 2) X(256, 256, 2, 2, 2) X(128, 128, 2, 4, 5)    \
+  X(128, 128, 4, 2, 5) X(256, 128, 4, 2, 5) X(128, 256, 2, 4, 5) X(64, 128, 2, 4, 5) X(64, 256, 1, 8, 5)
 
 #define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
 #define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
@@ -1494,6 +1626,17 @@ static int launch_conv(const Plan& pl, hipStream_t st) {
 
 static int elem_bytes_of(int dtype) { return dtype == SSIP_BF16 ? 2 : 4; }
 
+// Register-staged kernel for a FWD/DGRAD GEMM view the LDS-DMA kernel does not
+// address: the strided DGRAD without its phase split, filters of > 32 taps.
+static void fallback_regstaged(Plan& pl) {
+  ConvArgs& a = pl.args;
+  pl.stages = 0;
+  a.phased = 0;
+  pick_tile(a.M, a.Ng, 2, pl);
+  a.tiles_n = ceil_div(a.Ng, pl.bn);
+  pl.grid = dim3(ceil_div(a.M, pl.bm) * a.tiles_n, 1, 1);
+}
+
 // Stride-2 DGRAD as four dense sub-problems, one per output parity phase:
 // phase (ph, pw) only meets the taps r = r0 + 2*ri, s = s0 + 2*si, so the
 // k-loop skips the 3/4 of (tap, pixel) pairs the plain implicit GEMM would
@@ -1545,14 +1688,18 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
   Plan pl;
   int rc = plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
+  if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
   SSIP_REQUIRE(x && w_krsc && y, SSIP_ERR_ARG, "ssip_conv_fwd: null pointer");
   pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
+  pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
+  pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_FWD, T>(pl, (hipStream_t)stream));
 }
 
 int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
   Plan pl;
   if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
+  if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
   return ceil_div(pl.args.M, pl.bm);
 }
 
@@ -1562,8 +1709,11 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
   phase_split(pl, d);
+  if (pl.stages > 0 && ((d->stride != 1 && !pl.args.phased) || d->R * d->S > 32)) fallback_regstaged(pl);
   SSIP_REQUIRE(dy && w_crsk && dx, SSIP_ERR_ARG, "ssip_conv_dgrad: null pointer");
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
+  pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
+  pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));
 }
 
@@ -1589,6 +1739,7 @@ int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const
   if (rc) return rc;
   SSIP_REQUIRE(dy && w_crsk && zmask && y && mean && invstd && dpre && partial, SSIP_ERR_ARG,
                "ssip_conv_dgrad_bn: null pointer");
+  if (pl.stages > 0 && (d->stride != 1 || d->R * d->S > 32)) fallback_regstaged(pl);  // not phase-split here
   if (pl.stages > 0 && !getenv("SSIP_CONV_FORCE")) {  // the fused epilogue is built for the 128-row tiles only
     pl.bm = 128; pl.wmw = 4; pl.wnw = 2; pl.stages = 2;
     pl.bn = (pl.args.Ng % 128 == 0) ? 128 : 64;
@@ -1597,6 +1748,8 @@ int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const
   }
   SSIP_REQUIRE(pl.bm >= 128, SSIP_ERR_ARG, "ssip_conv_dgrad_bn: partial sizing assumes >= 128-row tiles");
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dpre; pl.args.add = dx_add;
+  pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
+  pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
   pl.args.pmask = zmask; pl.args.py = y; pl.args.pmean = mean; pl.args.pinvstd = invstd; pl.args.partial = partial;
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));
 }
@@ -1622,6 +1775,8 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
                (long long)workspace_bytes, (long long)need);
   SSIP_REQUIRE(c_real >= 1 && c_real <= d->C && s_real >= 1 && s_real <= d->S, SSIP_ERR_ARG, "bad c_real/s_real");
   pl.args.A = dy; pl.args.B = x; pl.args.out = workspace;
+  pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
+  pl.args.b_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, rc = launch_conv<MODE_WGRAD, T>(pl, st));
   if (rc) return rc;

@@ -16,12 +16,15 @@ FD = [(256, 128, 4, 2, 3), (256, 128, 4, 2, 2), (256, 64, 4, 1, 2), (256, 64, 4,
       (128, 64, 2, 2, 2), (128, 64, 2, 2, 3), (128, 64, 2, 1, 2), (128, 64, 4, 2, 2), (128, 128, 4, 4, 2),
       (256, 128, 4, 4, 2), (128, 64, 4, 2, 3), (128, 128, 4, 4, 3), (256, 128, 4, 4, 3),
       (256, 128, 2, 2, 2), (512, 64, 4, 1, 2), (256, 256, 2, 2, 2), (256, 256, 4, 2, 2), (512, 64, 8, 1, 2),
+      (256, 128, 4, 2, 5), (512, 64, 8, 1, 5), (128, 128, 4, 2, 5), (256, 64, 8, 1, 5),
       (256, 128, 4, 2, 0), (256, 64, 4, 2, 0), (128, 128, 2, 2, 0), (128, 64, 2, 2, 0)]
 WG = [(128, 128, 2, 2, 2), (128, 128, 2, 2, 3), (128, 128, 2, 4, 2), (128, 128, 2, 4, 3), (128, 64, 2, 2, 2),
       (128, 64, 2, 2, 3), (128, 64, 2, 1, 2), (64, 128, 1, 4, 2), (64, 128, 1, 4, 3), (64, 128, 1, 2, 2),
       (64, 128, 1, 8, 3), (128, 128, 4, 2, 2), (128, 128, 4, 4, 2), (128, 64, 2, 4, 2), (64, 128, 2, 4, 2),
       (64, 128, 1, 8, 2), (128, 128, 4, 4, 3), (64, 128, 2, 4, 3), (128, 64, 2, 4, 3), (256, 128, 4, 4, 2),
       (128, 256, 2, 2, 2), (256, 128, 2, 2, 2), (64, 256, 1, 2, 2), (256, 256, 2, 2, 2),
+      (128, 128, 2, 4, 5), (128, 128, 4, 2, 5), (256, 128, 4, 2, 5), (128, 256, 2, 4, 5), (64, 128, 2, 4, 5),
+      (64, 256, 1, 8, 5),
       (128, 128, 2, 2, 0), (128, 64, 2, 2, 0), (64, 128, 2, 2, 0)]
 
 

@@ -72,12 +72,12 @@ class GradBucketer:
             lo = min(spans[i][0] for i in idxs)
             hi = max(spans[i][0] + spans[i][1] for i in idxs)
             self.ranges.append((lo, hi))
-        # hipGraph mode (SemiStep(graph=True)): while the backward is being
-        # captured a completed bucket records an external event instead of
-        # launching; after each replay launch_after_graph() issues the
-        # all-reduces, each on the comm stream behind its bucket's event
+        # hipGraph mode (SemiStep(graph=True)): the backward is captured
+        # without collectives (ROCm allows no external event nodes in a graph,
+        # so a bucket cannot signal mid-replay); after each replay
+        # launch_after_graph() all-reduces the buckets in backward order on a
+        # comm stream behind the replay
         self.capture_mode = False
-        self.events: List[Optional[torch.cuda.Event]] = [None] * len(buckets)
         self._comm = None
         self.reset()
 
@@ -91,9 +91,6 @@ class GradBucketer:
             return
         self.launched[b] = True
         if self.capture_mode:
-            ev = torch.cuda.Event(external=True)
-            ev.record()
-            self.events[b] = ev
             return
         lo, hi = self.ranges[b]
         if self.world > 1:
@@ -101,22 +98,18 @@ class GradBucketer:
                                                 async_op=True))
 
     def end_capture(self) -> None:
-        """Record the events of buckets still open at the end of the captured backward."""
-        for b in range(len(self.buckets)):
-            if any(self.params[i].requires_grad for i in self.buckets[b]):
-                self._launch(b)
+        """Close the capture-time bookkeeping (nothing was launched)."""
+        self.launched = [True] * len(self.buckets)
 
     def launch_after_graph(self) -> None:
-        """Issue every bucket's all-reduce behind the event its gradients'
-        last kernel records inside the replayed graph."""
+        """All-reduce every bucket with trainable parameters, in backward
+        order, on the comm stream once the replayed backward is done."""
         if self._comm is None:
             self._comm = torch.cuda.Stream()
+        self._comm.wait_stream(torch.cuda.current_stream())
         self.handles = []
-        for b, ev in enumerate(self.events):
-            if ev is None:
-                continue
-            self._comm.wait_event(ev)
-            if self.world > 1:
+        for b in range(len(self.buckets)):
+            if self.world > 1 and any(self.params[i].requires_grad for i in self.buckets[b]):
                 lo, hi = self.ranges[b]
                 with torch.cuda.stream(self._comm):
                     self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM,

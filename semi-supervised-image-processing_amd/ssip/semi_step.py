@@ -47,9 +47,9 @@ class SemiStep:
     buffers and replays it: no per-kernel host launch cost, no host gaps.
     AdamW runs after the replay with its schedule on the device
     (``AdamW.use_device_schedule``); with world > 1 the gradient buckets are
-    all-reduced between the replay and AdamW, each bucket waiting only on
-    the external event the graph records when its gradients are complete, so
-    RCCL still overlaps the rest of the backward.
+    all-reduced between the replay and AdamW (ROCm has no external event
+    nodes, so a bucket cannot be released from inside the graph; ``--eager``
+    keeps the in-backward overlap instead).
     """
 
     def __init__(self, model: SSIPResNet, lr: float = 1e-4, weight_decay: float = 1e-4, tau: float = 0.7,

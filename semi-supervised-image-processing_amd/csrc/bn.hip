@@ -21,61 +21,40 @@
 
 namespace {
 
-// One workgroup (1024 threads) per channel, one pass over the per-tile
-// {count, sum, M2} records: each thread folds its tiles with Chan's parallel
-// update in fp64, then a fixed-order tree merges the 1024 partial states.
-__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
-  const double nn = n + nb;
-  if (nn <= 0.0) return;
-  const double d = meanb - mean;
-  mean += d * (nb / nn);
-  m2 += m2b + d * d * (n * nb / nn);
-  n = nn;
-}
-
+// One 1024-thread workgroup per channel, two passes over the per-tile
+// {count, sum, M2-about-tile-mean} records in fp64: the global mean from the
+// counts and sums, then M2 = sum_t M2_t + n_t (mean_t - mean)^2.  Threads
+// take records t = tid, tid + 1024, ...; wave butterflies and a 16-entry LDS
+// combine in fixed order keep the result reproducible.
 __global__ void __launch_bounds__(1024) bn_finalize_kernel(int C, int tiles, const float* __restrict__ partial,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* running_mean,
                                                            float* running_var, float momentum, float eps,
                                                            int update_running, float* mean_out, float* invstd_out,
                                                            float* scale_out, float* shift_out) {
+  __shared__ double sh[2][16];
   const int c = blockIdx.x;
-  __shared__ double sn[1024], sm[1024], s2[1024];
-  double n = 0.0, mean = 0.0, m2 = 0.0;
   const float* rec = partial + (long)c * tiles * 3;
-  int t = threadIdx.x;
-  // 4 records in flight per thread
-  for (; t + 3 * 1024 < tiles; t += 4 * 1024) {
-    float r[4][3];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) r[u][v] = rec[(long)(t + u * 1024) * 3 + v];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (r[u][0] > 0.f) chan_merge(n, mean, m2, r[u][0], (double)r[u][1] / r[u][0], r[u][2]);
+  double n = 0.0, sum = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += 1024) {
+    n += (double)rec[(long)t * 3];
+    sum += (double)rec[(long)t * 3 + 1];
   }
-  for (; t < tiles; t += 1024) {
-    const float nb = rec[(long)t * 3], sb = rec[(long)t * 3 + 1], mb = rec[(long)t * 3 + 2];
-    if (nb > 0.f) chan_merge(n, mean, m2, nb, (double)sb / nb, mb);
-  }
-  sn[threadIdx.x] = n;
-  sm[threadIdx.x] = mean;
-  s2[threadIdx.x] = m2;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      double a = sn[threadIdx.x], am = sm[threadIdx.x], a2 = s2[threadIdx.x];
-      chan_merge(a, am, a2, sn[threadIdx.x + o], sm[threadIdx.x + o], s2[threadIdx.x + o]);
-      sn[threadIdx.x] = a;
-      sm[threadIdx.x] = am;
-      s2[threadIdx.x] = a2;
+  n = block_sum_f64_1024(n, sh[0]);
+  sum = block_sum_f64_1024(sum, sh[1]);
+  const double mu = n > 0.0 ? sum / n : 0.0;
+  double m2 = 0.0;
+  for (int t = threadIdx.x; t < tiles; t += 1024) {
+    const double nb = rec[(long)t * 3];
+    if (nb > 0.0) {
+      const double d = (double)rec[(long)t * 3 + 1] / nb - mu;
+      m2 += (double)rec[(long)t * 3 + 2] + nb * d * d;
     }
-    __syncthreads();
   }
+  m2 = block_sum_f64_1024(m2, sh[0]);
   if (threadIdx.x == 0) {
-    const double N = sn[0], mu = sm[0];
-    const double var = s2[0] / N;
+    const double N = n;
+    const double var = m2 / N;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
     const float scale = g * invstd;
@@ -84,7 +63,7 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(int C, int tiles, con
     scale_out[c] = scale;
     shift_out[c] = b - (float)mu * scale;
     if (update_running) {
-      const double unbiased = N > 1 ? s2[0] / (N - 1) : var;
+      const double unbiased = N > 1 ? m2 / (N - 1) : var;
       running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
     }
@@ -369,7 +348,7 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, (const T*)y, mean, invstd, mscale, mshift, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, blocks, (long)M, partial, gamma, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, (long)M, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
                        (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
@@ -386,7 +365,7 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                "ssip_bn_bwd_from_partials: unsupported size");
   hipStream_t st = (hipStream_t)stream;
   const int total8 = (int)(M * C / 8);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, tiles, (long)M, partial, gamma, mean,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, tiles, (long)M, partial, gamma, mean,
                      invstd, dgamma, dbeta, accumulate, coef);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,

@@ -121,12 +121,39 @@ __global__ void avgpool_fc_fwd_kernel(int PQ, int C, int J, const T* __restrict_
   float* red = sfeat + C;
   const T* zb = z + (long)b * PQ * C;
   const float inv = 1.f / (float)PQ;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f;
-    for (int i = 0; i < PQ; ++i) a += to_f32<T>(zb[(long)i * C + c]);
-    const float f = a * inv;
-    sfeat[c] = f;
-    if (feat) feat[(long)b * C + c] = f;
+  const int cpr = C >> 3;
+  if ((C & 7) == 0 && cpr <= 256 && 256 % cpr == 0) {
+    // 16-B vectors: thread (group g, chunk k) sums rows g, g + G, ... of its
+    // 8 channels; the G group partials are combined in order through LDS
+    const int G = 256 / cpr, k = threadIdx.x % cpr, g = threadIdx.x / cpr;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int i = g; i < PQ; i += G) {
+      Vec8<T> v;
+      v.load(zb + (long)i * C + k * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v.get(j);
+    }
+    float* part = red;  // [G][C] after sfeat[C]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[g * C + k * 8 + j] = acc[j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float t = 0.f;
+      for (int q = 0; q < G; ++q) t += part[q * C + c];
+      const float f = t * inv;
+      sfeat[c] = f;
+      if (feat) feat[(long)b * C + c] = f;
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float t = 0.f;
+      for (int i = 0; i < PQ; ++i) t += to_f32<T>(zb[(long)i * C + c]);
+      const float f = t * inv;
+      sfeat[c] = f;
+      if (feat) feat[(long)b * C + c] = f;
+    }
   }
   __syncthreads();
   if (!logits) return;
@@ -160,21 +187,24 @@ __global__ void avgpool_fc_bwd_data_kernel(int PQ, int C, int J, const float* __
 }
 
 // dW[j][c] (+)= sum_b dlogits[b][j] feat[b][c];  dbias[j] (+)= sum_b dlogits[b][j]
-// block = 64 output elements x 4 batch groups; fixed-order LDS combine.
-__global__ void fc_bwd_weight_kernel(int B, int C, int J, const float* __restrict__ dlogits,
-                                     const float* __restrict__ feat, float* dw, float* dbias, int accumulate) {
-  __shared__ float red[4][64];
+// block = 64 output elements x 16 batch groups; fixed-order LDS combine.
+__global__ void __launch_bounds__(1024) fc_bwd_weight_kernel(int B, int C, int J, const float* __restrict__ dlogits,
+                                                             const float* __restrict__ feat, float* dw, float* dbias,
+                                                             int accumulate) {
+  __shared__ float red[16][65];
   const int cl = threadIdx.x & 63, bg = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + cl;
   float a = 0.f;
   if (i < J * C) {
     const int j = i / C, c = i % C;
-    for (int b = bg; b < B; b += 4) a += dlogits[(long)b * J + j] * feat[(long)b * C + c];
+    for (int b = bg; b < B; b += 16) a += dlogits[(long)b * J + j] * feat[(long)b * C + c];
   }
   red[bg][cl] = a;
   __syncthreads();
   if (bg == 0 && i < J * C) {
-    const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][cl];
     dw[i] = accumulate ? dw[i] + t : t;
   }
   if (dbias && blockIdx.x == 0 && threadIdx.x < J) {
@@ -336,7 +366,7 @@ int ssip_avgpool_fc_fwd(int dtype, int B, int PQ, int C, int J, const void* z, c
                         float* feat, float* logits, void* stream) {
   SSIP_REQUIRE(B > 0 && PQ > 0 && C > 0 && z && (feat || logits), SSIP_ERR_ARG, "ssip_avgpool_fc_fwd: bad arguments");
   SSIP_REQUIRE(!logits || (w && J > 0), SSIP_ERR_ARG, "ssip_avgpool_fc_fwd: fc weight required");
-  const size_t shm = (size_t)(C + 256) * sizeof(float);
+  const size_t shm = (size_t)(C + 2048) * sizeof(float);  // sfeat[C] + the group partials (<= 2048)
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(avgpool_fc_fwd_kernel<T>, dim3(B), dim3(256), shm, (hipStream_t)stream, PQ, C, J, (const T*)z,
                        w, bias, feat, logits);
@@ -356,7 +386,7 @@ int ssip_avgpool_fc_bwd(int dtype, int B, int PQ, int C, int J, const float* dlo
   if (dw) {
     SSIP_REQUIRE(feat, SSIP_ERR_ARG, "ssip_avgpool_fc_bwd: feat required for dw");
     SSIP_REQUIRE(J <= 256, SSIP_ERR_ARG, "ssip_avgpool_fc_bwd: J <= 256");
-    hipLaunchKernelGGL(fc_bwd_weight_kernel, dim3((J * C + 63) / 64), dim3(256), 0, st, B, C, J, dlogits, feat, dw,
+    hipLaunchKernelGGL(fc_bwd_weight_kernel, dim3((J * C + 63) / 64), dim3(1024), 0, st, B, C, J, dlogits, feat, dw,
                        dbias, accumulate);
   }
   return ::ssip::check_launch("avgpool_fc_bwd");

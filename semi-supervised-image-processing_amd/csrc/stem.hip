@@ -331,7 +331,7 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                        pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(1024), 0, st, C, blocks, M, partial, gamma, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, M, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
                        (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);

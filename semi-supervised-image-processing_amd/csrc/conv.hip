@@ -85,6 +85,10 @@ struct ConvArgs {
   PhaseInfo phase[4];
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
   uint32_t a_bytes, b_bytes;  // operand extents (LDS-DMA kernel buffer resources)
+  // WGRAD x-gather walk: a 64-row k-step advances each row's output pixel
+  // (n, p, q) by (dn, dp, dq); its input byte offset by k0, plus e1 when q
+  // wraps into the next row and e2 when p wraps into the next image
+  int wg_dn, wg_dp, wg_dq, wg_k0, wg_e1, wg_e2;
 };
 
 template <typename T> struct Traits;
@@ -1056,6 +1060,35 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
 #pragma unroll
     for (int t = 0; t < LA; ++t) a_off[t] = (uint32_t)(((mstart + a_h[t]) * a.K + a_c[t]) * 2);
   }
+  // WGRAD x gather: per slot the output pixel (p, q) of its row, the byte
+  // offset of its tap's input pixel (+ channel chunk), and the p / q ranges
+  // for which that tap lies inside the image (fixed: the slot's tap is fixed)
+  int w_p[LB], w_q[LB], w_plo[LB], w_pn[LB], w_qlo[LB], w_qn[LB];
+  uint32_t w_pix[LB];
+  if constexpr (WG) {
+#pragma unroll
+    for (int t = 0; t < LB; ++t) {
+      const int m = (int)min(mstart + b_row[t], (long)a.Mred - 1);
+      const int n = fdiv(m, a.div_pq);
+      const int rem = m - n * a.P * a.Q;
+      const int pp = fdiv(rem, a.div_q);
+      const int qq = rem - pp * a.Q;
+      w_p[t] = pp;
+      w_q[t] = qq;
+      const int hin = pp * a.stride - a.pad + b_r[t], win = qq * a.stride - a.pad + b_s[t];
+      w_pix[t] = (uint32_t)(((((long)n * a.H + hin) * a.W + win) * a.C + b_c[t]) * 2);
+      // hin = p*stride - pad + r in [0, H)  <=>  p in [plo, plo + pn)
+      const int r0 = a.pad - b_r[t], s0 = a.pad - b_s[t];
+      const int plo = r0 > 0 ? (r0 + a.stride - 1) / a.stride : 0;
+      const int phi = min(a.P, (a.H - 1 + r0) >= 0 ? (a.H - 1 + r0) / a.stride + 1 : 0);
+      const int qlo = s0 > 0 ? (s0 + a.stride - 1) / a.stride : 0;
+      const int qhi = min(a.Q, (a.W - 1 + s0) >= 0 ? (a.W - 1 + s0) / a.stride + 1 : 0);
+      w_plo[t] = plo;
+      w_pn[t] = b_ok[t] ? max(0, phi - plo) : 0;
+      w_qlo[t] = qlo;
+      w_qn[t] = max(0, qhi - qlo);
+    }
+  }
 
   auto issue = [&](int ks, int stage) {
     char* As = smem + stage * STAGE;
@@ -1113,19 +1146,19 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
       }
 #pragma unroll
       for (int t = 0; t < LB; ++t) {
-        const long m = mstart + (long)ks * BK + b_row[t];
-        const bool mok = b_ok[t] && m < mend;
-        const int mm = mok ? (int)m : 0;
-        const int n = fdiv(mm, a.div_pq);
-        const int rem = mm - n * a.P * a.Q;
-        const int p = fdiv(rem, a.div_q);
-        const int q = rem - p * a.Q;
-        const int hin = p * a.stride - a.pad + b_r[t];
-        const int win = q * a.stride - a.pad + b_s[t];
-        const bool ok = mok && hin >= 0 && hin < a.H && win >= 0 && win < a.W;
-        const T* src = ok ? Bg + ((long)((n * a.H + hin) * a.W + win)) * a.C + b_c[t]
-                          : reinterpret_cast<const T*>(g_zero16);
-        glds16(src, Bs + (wave + NW * t) * 1024);
+        const bool ok = b_row[t] < mlim && (uint32_t)(w_p[t] - w_plo[t]) < (uint32_t)w_pn[t] &&
+                        (uint32_t)(w_q[t] - w_qlo[t]) < (uint32_t)w_qn[t];
+        blds16(rsB, ok ? w_pix[t] : SSIP_OOB, Bs + (wave + NW * t) * 1024);
+        // advance the slot's row by the 64 rows of a k-step
+        int q = w_q[t] + a.wg_dq;
+        const bool c1 = q >= a.Q;
+        q = c1 ? q - a.Q : q;
+        int pp = w_p[t] + a.wg_dp + (c1 ? 1 : 0);
+        const bool c2 = pp >= a.P;
+        pp = c2 ? pp - a.P : pp;
+        w_q[t] = q;
+        w_p[t] = pp;
+        w_pix[t] += (uint32_t)(a.wg_k0 + (c1 ? a.wg_e1 : 0) + (c2 ? a.wg_e2 : 0));
       }
     }
     if constexpr (!WG) {
@@ -1777,6 +1810,17 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   pl.args.A = dy; pl.args.B = x; pl.args.out = workspace;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
+  {
+    const int PQ = d->P * d->Q, BKr = 64;  // LDS-DMA k-step rows (bf16)
+    const int dn = BKr / PQ, rem = BKr % PQ;
+    ConvArgs& g = pl.args;
+    g.wg_dn = dn;
+    g.wg_dp = rem / d->Q;
+    g.wg_dq = rem % d->Q;
+    g.wg_k0 = (dn * d->H * d->W + g.wg_dp * d->stride * d->W + g.wg_dq * d->stride) * d->C * 2;
+    g.wg_e1 = (d->stride * d->W - d->Q * d->stride) * d->C * 2;
+    g.wg_e2 = (d->H * d->W - d->P * d->stride * d->W) * d->C * 2;
+  }
   hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, rc = launch_conv<MODE_WGRAD, T>(pl, st));
   if (rc) return rc;

@@ -56,6 +56,7 @@ def parse():
 def main():
     args = parse()
     from ssip import SSIPResNet, ops, replace_fc
+    from ssip import resnet as resnet_mod
     from ssip.dist import GradBucketer, init_from_env
     from ssip.semi_step import SemiStep
 
@@ -109,8 +110,10 @@ def main():
     timer = ops.ConvTimer()
     ops.set_conv_timer(timer)
     graph, step.graph = step.graph, False  # the same kernels launched one by one, each bracketed by events
+    side, resnet_mod.WGRAD_SIDE_STREAM = resnet_mod.WGRAD_SIDE_STREAM, False  # wgrads timed without overlap
     step(x_l, y_l, x_u)
     step.graph = graph
+    resnet_mod.WGRAD_SIDE_STREAM = side
     ops.set_conv_timer(None)
     summ = timer.summary()
     conv_flops = sum(v[0] for v in summ.values())

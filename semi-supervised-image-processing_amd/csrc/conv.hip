@@ -1373,6 +1373,323 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
+// Halo-resident 3x3 / stride 1 / pad 1 convolution over 64 reduction
+// channels: every forward conv of ResNet layer1 and every stride-1 DGRAD
+// whose reduction is 64 channels (the same conv of dy with the taps flipped).
+//
+// The implicit-GEMM kernel above gathers the A operand once per tap (each
+// input pixel crosses L2 -> LDS nine times) and pays a barrier per k-step.
+// Here a persistent workgroup (one per CU) keeps the whole 64-column weight
+// panel (9 taps x 64 x 64 bf16 = 72 KiB) resident in LDS and stages, per
+// tile of TR whole output rows (TR*W <= 256 pixels of one image), the
+// (TR+2) x (W+2) zero-haloed input rows once.  Tap (r, s) of output pixel
+// (j, q) is LDS pixel (j + r)(W+2) + q + s, a uniform offset from tap (0, 0),
+// so the nine taps are nine shifted fragment reads of one LDS image and the
+// 18 MFMA k-steps of a tile run with no barrier.  The input rows are double
+// buffered: tile u+1's rows are DMA'd while tile u computes, and tile u's
+// epilogue stages its output through its own (then idle) buffer.  The wait
+// for the next rows is a counted vmcnt that leaves the epilogue's stores in
+// flight (vector-memory ops retire in issue order; the epilogue issues a
+// fixed number of them per thread through buffer ops, rows past the tile
+// going to an out-of-range offset).  LDS pixels use ktile_off's 16-B slot
+// swizzle (conflict-free ds_read_b128 over 16 consecutive pixels).  Each
+// MFMA k-step is one weight tap's 64 channels, in tap order, exactly as in
+// conv_glds_kernel: the outputs are the same bits.
+//
+// FWD epilogue: bf16 y plus the BatchNorm statistics of the workgroup's
+// tiles merged in fixed order (Chan) into one {count, sum, M2} record per
+// (channel, workgroup): [Ncols][G][3].  DGRAD epilogue: dx (+ add, which may
+// alias dx).
+// ---------------------------------------------------------------------------
+struct HaloArgs {
+  const __bf16* X;    // [N][H][W][64]   (FWD: x, DGRAD: dy)
+  const __bf16* Wt;   // [Ncols][9][64]  (FWD: w_krsc, DGRAD: w_crsk)
+  __bf16* out;        // [N][H][W][Ncols]
+  const __bf16* add;  // DGRAD residual gradient (nullable, may alias out)
+  float* partial;     // FWD BN records (nullable)
+  uint32_t x_bytes, w_bytes, o_bytes;
+  int N, H, W, Ncols, TR, tiles, units, flip;
+  int dbg;  // ablation (tools/time_halo.py): 1 = no MFMA, 2 = no epilogue
+};
+
+constexpr int HALO_XBUF = 44 * 1024;
+constexpr int HALO_WMW = 4;
+
+// X-row LDS image: pixel px's 128-B row, 16-B slot s at s ^ 2((px >> 1) & 3).
+// Fragment reads start at any pixel (tap shifts); with this swizzle the 16
+// lanes of every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows
+// r0..r0+15 across two k-slots) hit 16 distinct 16-B bank slots for every r0
+// (ktile_off's swizzle is conflict-free only for r0 = 0 mod 16).
+__device__ __forceinline__ int xtile_off(int px, int slot) { return px * 128 + ((slot ^ (((px >> 1) & 3) << 1)) << 4); }  // wave rows of every conv_halo_kernel instantiation (BN record count)
+
+// LDS-only workgroup barrier: __syncthreads() would also drain vmcnt, i.e.
+// wait for the next tile's rows in flight and this tile's output stores
+__device__ __forceinline__ void halo_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }  // one input-row buffer: (TR + 2) * (W + 2) <= 352 pixels
+
+template <int WMW, int WNW>
+__global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
+  typedef __bf16 T;
+  constexpr int NW = WMW * WNW, NT = 64 * NW;
+  constexpr int BM = 256, BN = 64;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW, FM = WTM / 16, FN = WTN / 16;
+  constexpr int B_BYTES = 9 * BN * 128;
+  static_assert(FM >= 1 && FN >= 1 && (NW == 4 || NW == 8), "bad halo wave tile");
+  static_assert(B_BYTES + 2 * HALO_XBUF <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[B_BYTES + 2 * HALO_XBUF];
+  char* const Bs = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int u0 = (int)((long)g * a.units / G), u1 = (int)((long)(g + 1) * a.units / G);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsW = make_rsrc(a.Wt, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t rsO = make_rsrc(a.out, a.o_bytes), rsA = make_rsrc(a.add, a.o_bytes);
+  const int Wp = a.W + 2;
+  const int npx = (a.TR + 2) * Wp;
+  const int nxi = (npx + 7) >> 3;  // X DMA wave-instructions per tile (8 pixels each)
+  const int rows = a.TR * a.W;     // output pixels per tile
+  const int mrows = a.TR * Wp;     // GEMM rows per tile: the padded grid (q = W, W+1 are discarded)
+
+  auto issue_x = [&](int tile, char* Xs) {
+    const int R0 = tile * a.TR;
+    const int n = R0 / a.H, p0 = R0 - n * a.H;
+    for (int i = wave; i < nxi; i += NW) {
+      const int px = i * 8 + (lane >> 3);
+      const int sr = px / Wp, sc = px - sr * Wp;
+      const int pin = p0 - 1 + sr, win = sc - 1;
+      const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
+      const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
+      const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
+      blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
+    }
+  };
+  auto issue_w = [&](int jn) {
+    for (int i = wave; i < 72; i += NW) {
+      const int tw = i >> 3, col = ((i & 7) << 3) + (lane >> 3);
+      const int ch = (lane & 7) ^ ((col >> 1) & 7);
+      const uint32_t off = (uint32_t)(((((long)jn * 64 + col) * 9 + tw) * 64 + ch * 8) * 2);
+      blds16(rsW, off, Bs + i * 1024);
+    }
+  };
+
+  // per-lane fragment bases: A rows (LDS pixel of tap (0, 0)), B columns
+  int pxb[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = wm * WTM + i * 16 + (lane & 15);
+    pxb[i] = m < mrows ? m : 0;  // row m of the padded grid reads LDS pixel m + tap offset
+  }
+  const int kq = lane >> 4;
+  int boff[FN][2];
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) boff[jj][kh] = ktile_off(wn * WTN + jj * 16 + (lane & 15), 4 * kh + kq);
+
+  // BN records [Ncols][G][WMW][3]: one per (channel, workgroup, wave row);
+  // zero this workgroup's, then lanes < 16 of each wave keep the running
+  // {n, mean, M2} of their FN columns over the wave's rows of every tile
+  if (a.partial) {
+    for (int c = tid; c < a.Ncols * WMW; c += NT) {
+      float* rec = a.partial + ((long)(c / WMW) * G * WMW + (long)g * WMW + c % WMW) * 3;
+      rec[0] = 0.f;
+      rec[1] = 0.f;
+      rec[2] = 0.f;
+    }
+  }
+  float st_n = 0.f, st_mean[FN], st_m2[FN];
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj) st_mean[jj] = st_m2[jj] = 0.f;
+  // this lane's output rows (rbase + 16 i + e): byte offset within a tile's
+  // output block and validity (q < W of the padded grid), fixed for all tiles
+  const int rbase = wm * WTM + kq * 4, cbase = wn * WTN + (lane & 15);
+  uint32_t rowoff[FM][4];
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = rbase + i * 16 + e;
+      const int j = m / Wp, q = m - j * Wp;
+      const bool v = m < mrows && q < a.W;
+      rowoff[i][e] = v ? (uint32_t)(((j * a.W + q) * a.Ncols + cbase) * 2) : 0x80000000u;  // + jj*32 stays out of range
+      vmask |= (v ? 1u : 0u) << (i * 4 + e);
+    }
+  int wrows = 0;  // valid rows of this wave in a tile (uniform)
+  for (int r = wm * WTM; r < wm * WTM + WTM; ++r) wrows += (r < mrows && r % Wp < a.W) ? 1 : 0;
+
+  if (u0 < u1) {
+    const int jn = u0 / a.tiles;
+    issue_w(jn);
+    issue_x(u0 - jn * a.tiles, smem + B_BYTES);
+  }
+  // One barrier per tile: after it every wave has finished the previous
+  // tile's fragment reads (so that buffer may take the next rows) and has
+  // seen its own share of this tile's rows land (the vmcnt(0) each wave
+  // issues after its MFMAs, by which time the prefetch has had the whole
+  // MFMA phase).  The epilogue writes straight from the accumulators with
+  // 16-bit buffer stores and needs no LDS, so a wave that finishes its MFMAs
+  // early runs its epilogue while the other waves still compute, and its
+  // stores stay in flight into the next tile.
+  bool first = true;
+  for (int u = u0; u < u1; ++u) {
+    const int jn = u / a.tiles, tile = u - jn * a.tiles;
+    char* const Xs = smem + B_BYTES + ((u - u0) & 1) * HALO_XBUF;
+    char* const Xn = smem + B_BYTES + ((u - u0 + 1) & 1) * HALO_XBUF;
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    first = false;
+    halo_lds_barrier();
+    const int un = u + 1;
+    const bool more = un < u1;
+    const int jn_next = more ? un / a.tiles : jn;
+    const bool prefetch = more && jn_next == jn;
+    if (prefetch) issue_x(un - jn * a.tiles, Xn);  // tile u-1's buffer: every wave is past its reads
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // 18 k-steps (weight tap t, 32-channel half kh) in weight-tap order, as
+    // conv_glds_kernel; DGRAD's tap t reads dy at the flipped shift 8 - t.
+    // Fragments are read one k-step ahead (register double buffer) so the
+    // LDS latency hides behind the previous step's MFMAs.
+    Frag<T> fa[2][FM], fb[2][FN];
+    auto load_step = [&](int st, Frag<T>(&ra)[FM], Frag<T>(&rb)[FN]) {
+      const int t = st >> 1, kh = st & 1;
+      const int tt = a.flip ? 8 - t : t;
+      const int toff = (tt / 3) * Wp + (tt % 3);
+      const char* bt = Bs + t * (BN * 128);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        ra[i].v = *reinterpret_cast<const bf16x8*>(Xs + xtile_off(pxb[i] + toff, 4 * kh + kq));
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) rb[jj].v = *reinterpret_cast<const bf16x8*>(bt + boff[jj][kh]);
+    };
+    if (a.dbg != 1) {
+      load_step(0, fa[0], fb[0]);
+#pragma unroll
+      for (int st = 0; st < 18; ++st) {
+        if (st + 1 < 18) load_step(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
+      }
+    }
+    // the next tile's rows (issued before the MFMAs) and this wave's older
+    // stores retire here; nothing younger is in flight
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.dbg == 2) {
+      if (more && !prefetch) {
+        halo_lds_barrier();
+        issue_w(jn_next);
+        issue_x(un - jn_next * a.tiles, Xn);
+        first = true;
+      }
+      continue;
+    }
+
+    // ---- epilogue
+    if (a.partial && wrows > 0) {
+      // per-wave statistics of this tile (fp32 accumulators, valid rows),
+      // merged into the wave's running record in tile order (Chan)
+      const float nt = (float)wrows;
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s += ((vmask >> (i * 4 + e)) & 1) ? acc[i][jj][e] : 0.f;
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mt = s / nt;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = acc[i][jj][e] - mt;
+            q += ((vmask >> (i * 4 + e)) & 1) ? d * d : 0.f;
+          }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (st_n == 0.f) {
+          st_mean[jj] = mt;
+          st_m2[jj] = q;
+        } else {
+          const float nn = st_n + nt, d = mt - st_mean[jj];
+          st_mean[jj] += d * (nt / nn);
+          st_m2[jj] += q + d * d * (st_n * nt / nn);
+        }
+      }
+      st_n += nt;
+      if (!prefetch) {  // the panel (or the workgroup's range) ends with this tile
+        if (lane < 16) {
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj) {
+            const int c = jn * BN + cbase + jj * 16;
+            float* rec = a.partial + ((long)c * G * WMW + (long)g * WMW + wm) * 3;
+            rec[0] = st_n;
+            rec[1] = st_mean[jj] * st_n;
+            rec[2] = st_m2[jj];
+          }
+        }
+        st_n = 0.f;
+      }
+    }
+    {
+      // 16-bit stores straight from the accumulators (lane: 4 rows x 1 column
+      // per fragment; padded-grid rows go to an out-of-range offset)
+      const uint32_t obase = (uint32_t)(((long)tile * rows * a.Ncols + jn * BN) * 2);
+      uint32_t off[FM][4];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) off[i][e] = obase + rowoff[i][e];
+      if (a.add) {
+        short r[FM][FN][4];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              r[i][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsA, off[i][e] + jj * 32, 0, 0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const T o = from_f32<T>(to_f32(from_f32<T>(acc[i][jj][e])) + to_f32(__builtin_bit_cast(T, r[i][jj][e])));
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off[i][e] + jj * 32, 0, 0);
+            }
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(acc[i][jj][e])), rsO,
+                                                    off[i][e] + jj * 32, 0, 0);
+      }
+    }
+    if (more && !prefetch) {
+      // panel change: new weights and the next tile's rows, loaded once every
+      // wave is past this tile's MFMAs
+      halo_lds_barrier();
+      issue_w(jn_next);
+      issue_x(un - jn_next * a.tiles, Xn);
+      first = true;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side planning
 // ---------------------------------------------------------------------------
 struct Plan {
@@ -1703,6 +2020,76 @@ static void phase_split(Plan& pl, const ssip_conv_desc* d) {
   pl.grid = dim3(std::max(1, max_tiles) * a.tiles_n, 4, 1);
 }
 
+// ---- halo path (conv_halo_kernel): 3x3 / stride 1 / pad 1, 64 reduction
+// channels, bf16.  SSIP_HALO=0 turns it off; an SSIP_CONV_FORCE for the pass
+// selects the implicit-GEMM kernels instead (tools/tune_conv.py).
+struct HaloPlan {
+  int TR, tiles, units, G, cols;
+};
+
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+              ? v
+              : 256;
+  }
+  return cus;
+}
+
+static bool halo_plan(int mode, const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
+  const char* e = getenv("SSIP_HALO");
+  if (e && e[0] == '0') return false;
+  const char* f = getenv("SSIP_CONV_FORCE");
+  if (f && f[0] == (mode == MODE_FWD ? 'f' : 'd')) return false;
+  if (dtype != SSIP_BF16 || !desc_ok(d) || d->R != 3 || d->S != 3 || d->stride != 1 || d->pad != 1 ||
+      d->P != d->H || d->Q != d->W)
+    return false;
+  const int redc = mode == MODE_FWD ? d->C : d->K;
+  const int cols = mode == MODE_FWD ? d->K : d->C;
+  if (redc != 64 || cols % 64 != 0) return false;
+  int TR = 0;
+  for (int tr = std::min(d->H, 256 / (d->W + 2)); tr >= 1; --tr)  // TR (W+2) GEMM rows <= 256
+    if (d->H % tr == 0 && (tr + 2) * (d->W + 2) <= HALO_XBUF / 128) {
+      TR = tr;
+      break;
+    }
+  if (TR == 0 || TR * d->W < 128) return false;  // short tiles: the implicit-GEMM kernels do better
+  const long pix = (long)d->N * d->H * d->W;
+  if (pix * 64 * 2 >= (1l << 31) || pix * cols * 2 >= (1l << 31)) return false;
+  hp.TR = TR;
+  hp.cols = cols;
+  hp.tiles = (int)((long)d->N * d->H / TR);
+  hp.units = hp.tiles * (cols / 64);
+  hp.G = std::min(hp.units, device_cus());
+  return true;
+}
+
+static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
+                       void* out, const void* add, float* partial, hipStream_t st) {
+  HaloArgs h;
+  h.X = static_cast<const __bf16*>(X);
+  h.Wt = static_cast<const __bf16*>(Wt);
+  h.out = static_cast<__bf16*>(out);
+  h.add = static_cast<const __bf16*>(add);
+  h.partial = partial;
+  h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 64 * 2);
+  h.w_bytes = (uint32_t)((long)hp.cols * 9 * 64 * 2);
+  h.o_bytes = (uint32_t)((long)d->N * d->H * d->W * hp.cols * 2);
+  h.N = d->N; h.H = d->H; h.W = d->W; h.Ncols = hp.cols;
+  h.TR = hp.TR; h.tiles = hp.tiles; h.units = hp.units;
+  h.flip = mode == MODE_DGRAD ? 1 : 0;
+  { const char* dbg = getenv("SSIP_HALO_DBG"); h.dbg = dbg ? atoi(dbg) : 0; }
+  const char* e = getenv("SSIP_HALO_WAVES");
+  if (e && atoi(e) == 4)
+    hipLaunchKernelGGL((conv_halo_kernel<4, 1>), dim3(hp.G), dim3(256), 0, st, h);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
+  return ::ssip::check_launch("conv_halo");
+}
+
 }  // namespace
 
 extern "C" {
@@ -1713,7 +2100,10 @@ int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d) {
   if (plan_conv(MODE_FWD, d, 4, pl) != SSIP_OK) {
     if (plan_conv(MODE_FWD, d, 2, pl) != SSIP_OK) return -1;
   }
-  return (int64_t)ceil_div(pl.args.M, 128) * d->K * 3;
+  int64_t n = (int64_t)ceil_div(pl.args.M, 128) * d->K * 3;
+  HaloPlan hp;  // one record per (channel, workgroup) on the halo path
+  if (halo_plan(MODE_FWD, d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
+  return n;
 }
 
 int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, void* y, float* bn_partial,
@@ -1723,6 +2113,9 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
   if (rc) return rc;
   if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
   SSIP_REQUIRE(x && w_krsc && y, SSIP_ERR_ARG, "ssip_conv_fwd: null pointer");
+  HaloPlan hp;
+  if (halo_plan(MODE_FWD, d, dtype, hp))
+    return launch_halo(MODE_FWD, d, hp, x, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream);
   pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
@@ -1730,6 +2123,8 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
 }
 
 int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
+  HaloPlan hp;
+  if (halo_plan(MODE_FWD, d, dtype, hp)) return hp.G * HALO_WMW;
   Plan pl;
   if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
   if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
@@ -1744,6 +2139,9 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   phase_split(pl, d);
   if (pl.stages > 0 && ((d->stride != 1 && !pl.args.phased) || d->R * d->S > 32)) fallback_regstaged(pl);
   SSIP_REQUIRE(dy && w_crsk && dx, SSIP_ERR_ARG, "ssip_conv_dgrad: null pointer");
+  HaloPlan hp;
+  if (halo_plan(MODE_DGRAD, d, dtype, hp))
+    return launch_halo(MODE_DGRAD, d, hp, dy, w_crsk, dx, dx_add, nullptr, (hipStream_t)stream);
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);

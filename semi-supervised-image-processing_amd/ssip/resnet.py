@@ -457,7 +457,38 @@ def _grad_target(p: torch.Tensor, arena) -> Tuple[torch.Tensor, bool]:
     return p.grad, True
 
 
+# Weight gradients sit off the backward's critical path (dout -> BN backward ->
+# dgrad -> next dout): they run on a second stream, forked from the main one
+# before each wgrad and joined at the end of the backward, so the HBM- and
+# latency-bound BN-backward passes and finalize launches overlap with them.
+# WGRAD_SIDE_STREAM = False serialises everything on the current stream.
+WGRAD_SIDE_STREAM = os.environ.get("SSIP_WGRAD_STREAM", "1") != "0"
+_side_streams = {}
+
+
+def _wgrad_stream(dev: torch.device):
+    if not WGRAD_SIDE_STREAM or dev.type != "cuda":
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _side_streams.get(idx)
+    if st is None:
+        st = _side_streams[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
 def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
+    side = _wgrad_stream(dlogits.device)
+    if side is None:
+        _backward_impl(model, sv, dlogits, None, None)
+        return
+    main = torch.cuda.current_stream(dlogits.device)
+    try:
+        _backward_impl(model, sv, dlogits, main, side)
+    finally:
+        main.wait_stream(side)
+
+
+def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, side):
     dt = sv.dtype
     N = sv.N
     arena = model._arena if (model._arena is not None and model._arena.valid()) else None
@@ -475,7 +506,15 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         dw, accw = _grad_target(fc_w, arena)
     if fc.bias is not None and fc.bias.requires_grad:
         db, accb = _grad_target(fc.bias, arena)
-    hook = getattr(model, "grad_ready_hook", None)
+    user_hook = getattr(model, "grad_ready_hook", None)
+    hook = user_hook
+    if user_hook is not None and side is not None:
+        def hook(params):
+            # the hook's consumers (gradient buckets) order themselves after
+            # the current stream: make that the side stream, joined to main
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                user_hook(params)
     if not trunk_trainable:
         if dw is not None:
             ops.avgpool_fc_bwd(dt, N, sv.last_pq, C, J, dlogits, fc_w.detach(), sv.feat, None, dw,
@@ -558,7 +597,13 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         if not w.requires_grad:
             return
         tgt, acc = _grad_target(w, arena)
-        ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
+        if side is None:
+            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
+            return
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
+        dy.record_stream(side)
 
     def conv_dgrad(rec: _ConvRec, dy, out, add=None):
         crsk = _prepped_t(model, rec)[1]

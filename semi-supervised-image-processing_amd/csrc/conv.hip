@@ -1690,6 +1690,225 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 }
 
 // ---------------------------------------------------------------------------
+// The stem conv (7x7 / stride 2 over the pre-padded 4-channel image, pad 0,
+// S padded to 8) in the same persistent, LDS-resident form.  A tile is
+// STEM_TR = 2 output rows; their 9 input rows (2 p0 .. 2 p0 + 8) are one
+// contiguous run of the NHWC4 image, DMA'd linearly into a double buffer.
+// Output pixel (j, q), filter row r reads the 8 pixels 2q .. 2q+7 of input
+// row 2j + r: 64 contiguous bytes = one 32-deep MFMA k-step (s = 7 carries a
+// zero weight), so a tile is 7 k-steps with no barrier.  GEMM rows are the
+// output rows padded to STEM_QP = 128 (q >= Q discarded).  The weight panel
+// (64 filters x 7 rows x 32) stays resident.  Epilogue as conv_halo_kernel:
+// 16-bit stores from the accumulators, per-wave BN records [K][G][4][3].
+// The k-order differs from conv_glds_kernel's C4 path (which pairs two filter
+// rows per 64-deep step), so outputs agree to fp32 rounding, not bitwise.
+// ---------------------------------------------------------------------------
+struct StemArgs {
+  const __bf16* X;    // [N][H][W][4]   pre-padded image
+  const __bf16* Wt;   // [Ncols][7][8][4]
+  __bf16* out;        // [N][P][Q][Ncols]
+  float* partial;     // BN records (nullable)
+  uint32_t x_bytes, w_bytes, o_bytes;
+  int N, H, W, P, Q, Ncols, tiles, units;
+};
+
+constexpr int STEM_QP = 128, STEM_TR = 2, STEM_XROWS = 2 * STEM_TR + 5;
+constexpr int STEM_XBUF = 17 * 1024;  // 9 rows x W x 8 B, W <= 240
+
+template <int WMW, int WNW>
+__global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_halo_kernel(const StemArgs a) {
+  typedef __bf16 T;
+  constexpr int NW = WMW * WNW, NT = 64 * NW;
+  constexpr int BM = STEM_TR * STEM_QP, BN = 64;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW, FM = WTM / 16, FN = WTN / 16;
+  constexpr int B_BYTES = 7 * BN * 64;  // [r][col][32 k], 16-B slot s at s ^ 2((col >> 3) & 1)
+  static_assert(FM >= 1 && FN >= 1, "bad stem wave tile");
+  __shared__ __attribute__((aligned(16))) char smem[B_BYTES + 2 * STEM_XBUF];
+  char* const Bs = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int u0 = (int)((long)g * a.units / G), u1 = (int)((long)(g + 1) * a.units / G);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsW = make_rsrc(a.Wt, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t rsO = make_rsrc(a.out, a.o_bytes);
+  const int xpitch = a.W * 8;                  // one input row (4 channels bf16)
+  const int xrun = STEM_XROWS * xpitch;        // bytes of a tile's input rows
+  const int nxi = (xrun + 1023) >> 10;         // 1-KiB DMA wave-instructions
+
+  auto issue_x = [&](int tile, char* Xs) {
+    const int R0 = tile * STEM_TR;
+    const int n = R0 / a.P, p0 = R0 - n * a.P;
+    const uint32_t base = (uint32_t)((((long)n * a.H + 2 * p0) * a.W) * 8);
+    for (int i = wave; i < nxi; i += NW) {
+      const int b = i * 1024 + lane * 16;
+      blds16(rsX, b < xrun ? base + (uint32_t)b : SSIP_OOB, Xs + i * 1024);
+    }
+  };
+  auto issue_w = [&](int jn) {
+    // 7 x 64 x 64 B = 28 KiB: instruction i covers rows r = i / 4, cols 16 (i % 4) .. +16
+    for (int i = wave; i < 28; i += NW) {
+      const int r = i >> 2, col = ((i & 3) << 4) + (lane >> 2);
+      const int sl = (lane & 3) ^ (((col >> 3) & 1) << 1);
+      const uint32_t off = (uint32_t)(((((long)jn * 64 + col) * 7 + r) * 32 + sl * 8) * 2);
+      blds16(rsW, off, Bs + i * 1024);
+    }
+  };
+
+  const int kq = lane >> 4;
+  const int rbase = wm * WTM + kq * 4, cbase = wn * WTN + (lane & 15);
+  // A fragment bases: GEMM row m = j * QP + q reads input row 2j + r, pixel 2q + 2kq
+  int abase[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = wm * WTM + i * 16 + (lane & 15);
+    const int j = m / STEM_QP, q = m - j * STEM_QP;
+    abase[i] = q < a.Q ? 2 * j * xpitch + (2 * q + 2 * kq) * 8 : 0;
+  }
+  int boff[FN];
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj) {
+    const int col = wn * WTN + jj * 16 + (lane & 15);
+    boff[jj] = col * 64 + ((kq ^ (((col >> 3) & 1) << 1)) << 4);
+  }
+  uint32_t rowoff[FM][4];
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = rbase + i * 16 + e;
+      const int j = m / STEM_QP, q = m - j * STEM_QP;
+      const bool v = q < a.Q;
+      rowoff[i][e] = v ? (uint32_t)(((j * a.Q + q) * a.Ncols + cbase) * 2) : 0x80000000u;
+      vmask |= (v ? 1u : 0u) << (i * 4 + e);
+    }
+  int wrows = 0;
+  for (int r = wm * WTM; r < wm * WTM + WTM; ++r) wrows += (r % STEM_QP < a.Q) ? 1 : 0;
+
+  if (a.partial) {
+    for (int c = tid; c < a.Ncols * WMW; c += NT) {
+      float* rec = a.partial + ((long)(c / WMW) * G * WMW + (long)g * WMW + c % WMW) * 3;
+      rec[0] = 0.f;
+      rec[1] = 0.f;
+      rec[2] = 0.f;
+    }
+  }
+  float st_n = 0.f, st_mean[FN], st_m2[FN];
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj) st_mean[jj] = st_m2[jj] = 0.f;
+
+  if (u0 < u1) {
+    const int jn = u0 / a.tiles;
+    issue_w(jn);
+    issue_x(u0 - jn * a.tiles, smem + B_BYTES);
+  }
+  bool first = true;
+  for (int u = u0; u < u1; ++u) {
+    const int jn = u / a.tiles, tile = u - jn * a.tiles;
+    char* const Xs = smem + B_BYTES + ((u - u0) & 1) * STEM_XBUF;
+    char* const Xn = smem + B_BYTES + ((u - u0 + 1) & 1) * STEM_XBUF;
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    first = false;
+    halo_lds_barrier();
+    const int un = u + 1;
+    const bool more = un < u1;
+    const int jn_next = more ? un / a.tiles : jn;
+    const bool prefetch = more && jn_next == jn;
+    if (prefetch) issue_x(un - jn * a.tiles, Xn);
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    Frag<T> fa[2][FM], fb[2][FN];
+    auto load_step = [&](int r, Frag<T>(&ra)[FM], Frag<T>(&rb)[FN]) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) ra[i].v = *reinterpret_cast<const bf16x8*>(Xs + abase[i] + r * xpitch);
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj)
+        rb[jj].v = *reinterpret_cast<const bf16x8*>(Bs + r * (BN * 64) + boff[jj]);
+    };
+    load_step(0, fa[0], fb[0]);
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      if (r + 1 < 7) load_step(r + 1, fa[(r + 1) & 1], fb[(r + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[r & 1][i], fb[r & 1][jj]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if (a.partial && wrows > 0) {
+      const float nt = (float)wrows;
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s += ((vmask >> (i * 4 + e)) & 1) ? acc[i][jj][e] : 0.f;
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mt = s / nt;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = acc[i][jj][e] - mt;
+            q += ((vmask >> (i * 4 + e)) & 1) ? d * d : 0.f;
+          }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (st_n == 0.f) {
+          st_mean[jj] = mt;
+          st_m2[jj] = q;
+        } else {
+          const float nn = st_n + nt, d = mt - st_mean[jj];
+          st_mean[jj] += d * (nt / nn);
+          st_m2[jj] += q + d * d * (st_n * nt / nn);
+        }
+      }
+      st_n += nt;
+      if (!prefetch) {
+        if (lane < 16) {
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj) {
+            const int c = jn * BN + cbase + jj * 16;
+            float* rec = a.partial + ((long)c * G * WMW + (long)g * WMW + wm) * 3;
+            rec[0] = st_n;
+            rec[1] = st_mean[jj] * st_n;
+            rec[2] = st_m2[jj];
+          }
+        }
+        st_n = 0.f;
+      }
+    }
+    {
+      const uint32_t obase = (uint32_t)(((long)tile * STEM_TR * a.Q * a.Ncols + jn * BN) * 2);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(acc[i][jj][e])), rsO,
+                                                  obase + rowoff[i][e] + jj * 32, 0, 0);
+    }
+    if (more && !prefetch) {
+      halo_lds_barrier();
+      issue_w(jn_next);
+      issue_x(un - jn_next * a.tiles, Xn);
+      first = true;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side planning
 // ---------------------------------------------------------------------------
 struct Plan {
@@ -2067,6 +2286,42 @@ static bool halo_plan(int mode, const ssip_conv_desc* d, int dtype, HaloPlan& hp
   return true;
 }
 
+// ---- stem path (conv_stem_halo_kernel): the pre-padded 7x7 / stride 2 stem
+static bool stem_plan(const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
+  const char* e = getenv("SSIP_HALO");
+  if (e && e[0] == '0') return false;
+  const char* f = getenv("SSIP_CONV_FORCE");
+  if (f && f[0] == 'f') return false;
+  if (dtype != SSIP_BF16 || !desc_ok(d) || d->C != 4 || d->R != 7 || d->S != 8 || d->stride != 2 || d->pad != 0 ||
+      d->K % 64 != 0 || d->Q > STEM_QP || d->P % STEM_TR != 0 || d->W % 2 != 0 ||
+      STEM_XROWS * d->W * 8 > STEM_XBUF || d->H < 2 * (d->P - 1) + 7)
+    return false;
+  const long ib = (long)d->N * d->H * d->W * 8, ob = (long)d->N * d->P * d->Q * d->K * 2;
+  if (ib >= (1l << 31) || ob >= (1l << 31)) return false;
+  hp.TR = STEM_TR;
+  hp.cols = d->K;
+  hp.tiles = d->N * d->P / STEM_TR;
+  hp.units = hp.tiles * (d->K / 64);
+  hp.G = std::min(hp.units, 2 * device_cus());  // 62 KiB of LDS: two workgroups per CU
+  return true;
+}
+
+static int launch_stem_halo(const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt, void* out,
+                            float* partial, hipStream_t st) {
+  StemArgs s;
+  s.X = static_cast<const __bf16*>(X);
+  s.Wt = static_cast<const __bf16*>(Wt);
+  s.out = static_cast<__bf16*>(out);
+  s.partial = partial;
+  s.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 8);
+  s.w_bytes = (uint32_t)((long)d->K * 7 * 8 * 4 * 2);
+  s.o_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
+  s.N = d->N; s.H = d->H; s.W = d->W; s.P = d->P; s.Q = d->Q; s.Ncols = d->K;
+  s.tiles = hp.tiles; s.units = hp.units;
+  hipLaunchKernelGGL((conv_stem_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, s);
+  return ::ssip::check_launch("conv_stem_halo");
+}
+
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
                        void* out, const void* add, float* partial, hipStream_t st) {
   HaloArgs h;
@@ -2103,6 +2358,7 @@ int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d) {
   int64_t n = (int64_t)ceil_div(pl.args.M, 128) * d->K * 3;
   HaloPlan hp;  // one record per (channel, workgroup) on the halo path
   if (halo_plan(MODE_FWD, d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
+  if (stem_plan(d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
   return n;
 }
 
@@ -2116,6 +2372,7 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp))
     return launch_halo(MODE_FWD, d, hp, x, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream);
+  if (stem_plan(d, dtype, hp)) return launch_stem_halo(d, hp, x, w_krsc, y, bn_partial, (hipStream_t)stream);
   pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
@@ -2125,6 +2382,7 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
 int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp)) return hp.G * HALO_WMW;
+  if (stem_plan(d, dtype, hp)) return hp.G * HALO_WMW;
   Plan pl;
   if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
   if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);

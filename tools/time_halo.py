@@ -47,3 +47,16 @@ for dbg in ("0", "1", "2"):
     t2 = time_fn(lambda: ops.conv_fwd(g, x, w, y, None), 20)
     print(f"ablation dbg={dbg}: stats {t:8.1f} us   nostats {t2:8.1f} us", flush=True)
 os.environ["SSIP_HALO_DBG"] = "0"
+
+# stem: 7x7 / stride 2 over the pre-padded NHWC4 image (conv_stem_halo_kernel vs the C4 GEMM path)
+for N in (256, 128):
+    g = ops.ConvGeom(N, 230, 230, 4, 64, 7, 8, 2, 0, 3, 7)
+    x = torch.randn(N, 230, 230, 4, device=dev).to(bf)
+    w = (torch.randn(64, 7, 8, 4, device=dev) * 0.05).to(bf)
+    y = torch.empty(N, 112, 112, 64, device=dev, dtype=bf)
+    part = torch.empty(ops.conv_fwd_partial_floats(g), device=dev)
+    for halo in ("1", "0"):
+        os.environ["SSIP_HALO"] = halo
+        t = time_fn(lambda: ops.conv_fwd(g, x, w, y, part), 20)
+        print(f"stem N={N} {'halo' if halo == '1' else 'gemm'} {t:8.1f} us {g.flops() / t / 1e6:7.0f} TF/s", flush=True)
+os.environ["SSIP_HALO"] = "1"

@@ -21,39 +21,39 @@
 
 namespace {
 
-// One 1024-thread workgroup per channel, two passes over the per-tile
-// {count, sum, M2-about-tile-mean} records in fp64: the global mean from the
-// counts and sums, then M2 = sum_t M2_t + n_t (mean_t - mean)^2.  Threads
-// take records t = tid, tid + 1024, ...; wave butterflies and a 16-entry LDS
-// combine in fixed order keep the result reproducible.
+// One 1024-thread workgroup per channel, one pass over the per-tile
+// {count, sum, M2-about-tile-mean} records in fp64, shifted by the first
+// record's mean K (the shifted-data form of the pairwise merge):
+//   n = sum n_t,  s = sum n_t (mean_t - K),  q = sum M2_t + n_t (mean_t - K)^2
+//   mean = K + s / n,  M2 = q - s^2 / n.
+// Threads take records t = tid, tid + 1024, ...; wave butterflies and a
+// 16-entry LDS combine in fixed order keep the result reproducible.
 __global__ void __launch_bounds__(1024) bn_finalize_kernel(int C, int tiles, const float* __restrict__ partial,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* running_mean,
                                                            float* running_var, float momentum, float eps,
                                                            int update_running, float* mean_out, float* invstd_out,
                                                            float* scale_out, float* shift_out) {
-  __shared__ double sh[2][16];
+  __shared__ double sh[3 * 16];
   const int c = blockIdx.x;
   const float* rec = partial + (long)c * tiles * 3;
-  double n = 0.0, sum = 0.0;
-  for (int t = threadIdx.x; t < tiles; t += 1024) {
-    n += (double)rec[(long)t * 3];
-    sum += (double)rec[(long)t * 3 + 1];
-  }
-  n = block_sum_f64_1024(n, sh[0]);
-  sum = block_sum_f64_1024(sum, sh[1]);
-  const double mu = n > 0.0 ? sum / n : 0.0;
-  double m2 = 0.0;
+  const double n0 = rec[0];
+  const double K = n0 > 0.0 ? (double)rec[1] / n0 : 0.0;
+  double v[3] = {0.0, 0.0, 0.0};
   for (int t = threadIdx.x; t < tiles; t += 1024) {
     const double nb = rec[(long)t * 3];
     if (nb > 0.0) {
-      const double d = (double)rec[(long)t * 3 + 1] / nb - mu;
-      m2 += (double)rec[(long)t * 3 + 2] + nb * d * d;
+      const double d = (double)rec[(long)t * 3 + 1] / nb - K;
+      v[0] += nb;
+      v[1] += nb * d;
+      v[2] += (double)rec[(long)t * 3 + 2] + nb * d * d;
     }
   }
-  m2 = block_sum_f64_1024(m2, sh[0]);
+  block_sums_f64_1024<3>(v, sh);
   if (threadIdx.x == 0) {
-    const double N = n;
+    const double N = v[0];
+    const double mu = N > 0.0 ? K + v[1] / N : 0.0;
+    const double m2 = N > 0.0 ? fmax(v[2] - v[1] * v[1] / N, 0.0) : 0.0;
     const double var = m2 / N;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const 
 // per-(row block, channel) sums of dout and dout*xhat.
 // Block: 256 threads; each thread owns an 8-channel chunk; threads/row = C/8.
 template <typename T>
-__global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T* __restrict__ dz,
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T* __restrict__ dz,
                                      const T* __restrict__ zmask, const T* __restrict__ y,
                                      const float* __restrict__ mean, const float* __restrict__ invstd,
                                      const float* __restrict__ mscale, const float* __restrict__ mshift,
@@ -156,21 +156,40 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
     load_f8(msc, mscale + c0);
     load_f8(msh, mshift + c0);
   }
-  if (rsub < rpi) {
-    for (long r = r0 + rsub; r < r1; r += rpi) {
-      Vec8<T> g, zz, yy;
-      g.load(dz + r * C + c0);
-      yy.load(y + r * C + c0);
-      if (zmask) zz.load(zmask + r * C + c0);
+  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& yy) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float d = g.get(j);
-        if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
-        if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
-        const float xh = (yy.get(j) - mu[j]) * is[j];
-        sd[j] += d;
-        sx[j] += d * xh;
+    for (int j = 0; j < 8; ++j) {
+      float d = g.get(j);
+      if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
+      if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
+      const float xh = (yy.get(j) - mu[j]) * is[j];
+      sd[j] += d;
+      sx[j] += d * xh;
+    }
+  };
+  if (rsub < rpi) {
+    // two rows in flight per thread; rows accumulate in the same order as a
+    // plain r += rpi walk, so the sums do not depend on the unroll
+    long r = r0 + rsub;
+    for (; r + rpi < r1; r += 2 * rpi) {
+      Vec8<T> g0, g1, z0, z1, y0, y1;
+      g0.load(dz + r * C + c0);
+      g1.load(dz + (r + rpi) * C + c0);
+      y0.load(y + r * C + c0);
+      y1.load(y + (r + rpi) * C + c0);
+      if (zmask) {
+        z0.load(zmask + r * C + c0);
+        z1.load(zmask + (r + rpi) * C + c0);
       }
+      acc(g0, z0, y0);
+      acc(g1, z1, y1);
+    }
+    if (r < r1) {
+      Vec8<T> g0, z0, y0;
+      g0.load(dz + r * C + c0);
+      y0.load(y + r * C + c0);
+      if (zmask) z0.load(zmask + r * C + c0);
+      acc(g0, z0, y0);
     }
   }
   __shared__ float red[2][256][9];
@@ -182,7 +201,8 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
   __syncthreads();
   // threads with rsub == 0 sum over rsub in fixed order
   if (threadIdx.x < cpr) {
-    float* out = partial + ((long)blockIdx.x * C + c0) * 2;
+    // [C][blocks][2]: each channel's records contiguous for the finalize
+    float* out = partial + ((long)c0 * gridDim.x + blockIdx.x) * 2;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = 0.f, b = 0.f;
@@ -190,8 +210,8 @@ __global__ void bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T*
         a += red[0][s * cpr + threadIdx.x][j];
         b += red[1][s * cpr + threadIdx.x][j];
       }
-      out[2 * j] = a;
-      out[2 * j + 1] = b;
+      out[(long)j * gridDim.x * 2] = a;
+      out[(long)j * gridDim.x * 2 + 1] = b;
     }
   }
 }
@@ -281,9 +301,9 @@ static int bn_elem_grid(long total8) {
 }
 
 static int bwd_rows_per_block(long M, int C) {
-  // aim for ~512 blocks, at least four full iterations of rows
+  // aim for ~2048 blocks (8 per CU), at least four full iterations of rows
   const int rpi = 256 / (C / 8);
-  long rows = (M + 511) / 512;
+  long rows = (M + 2047) / 2048;
   if (rows < 4 * rpi) rows = 4 * rpi;
   if (rows < rpi) rows = rpi;
   rows = ((rows + rpi - 1) / rpi) * rpi;
@@ -348,7 +368,7 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, (const T*)y, mean, invstd, mscale, mshift, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, (long)M, partial, gamma, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, (long)M, 1, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
                        (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
@@ -365,7 +385,7 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                "ssip_bn_bwd_from_partials: unsupported size");
   hipStream_t st = (hipStream_t)stream;
   const int total8 = (int)(M * C / 8);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, tiles, (long)M, partial, gamma, mean,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, tiles, (long)M, 0, partial, gamma, mean,
                      invstd, dgamma, dbeta, accumulate, coef);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,

@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_reduce_kernel(
   __syncthreads();
   const int rpi = blockDim.x / cpr;
   if (threadIdx.x < cpr) {
-    float* o = partial + ((long)blockIdx.x * C + c0) * 2;
+    float* o = partial + ((long)c0 * gridDim.x + blockIdx.x) * 2;  // [C][blocks][2]
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = 0.f, b = 0.f;
@@ -238,8 +238,8 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_reduce_kernel(
         a += red[0][q * cpr + threadIdx.x][j];
         b += red[1][q * cpr + threadIdx.x][j];
       }
-      o[2 * j] = a;
-      o[2 * j + 1] = b;
+      o[(long)j * gridDim.x * 2] = a;
+      o[(long)j * gridDim.x * 2 + 1] = b;
     }
   }
 }
@@ -331,7 +331,7 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                        pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, M, partial, gamma, mean,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, M, 1, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
                        (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);

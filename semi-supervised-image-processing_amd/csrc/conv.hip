@@ -1909,6 +1909,134 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
 }
 
 // ---------------------------------------------------------------------------
+// WGRAD of the same 3x3 / stride 1 / pad 1 convs with C = K = 64 (layer1):
+//   dW[k][(t, c)] = sum_m dy[m][k] * x_pad[m + toff(t)][c]
+// over the padded-grid rows m = j (W+2) + q of each tile (dy is zero at
+// q >= W).  A persistent workgroup (one per CU) stages per tile the input
+// rows (as conv_halo_kernel, with the m-major MTile swizzle) and the tile's
+// dy rows, both double-buffered, and keeps the whole 64 x 576 fp32 result in
+// registers across its tiles (waves: 2 k-halves x 4 quarters of the 36
+// (tap, 16-channel) column blocks); the nine taps are shifted transposed
+// fragment reads of the one input image.  At the end each workgroup writes
+// its partial dW as one fp32 slab; wgrad_reduce_kernel sums the slabs in
+// fixed order (deterministic).
+// ---------------------------------------------------------------------------
+struct HaloWgArgs {
+  const __bf16* X;   // [N][H][W][64]
+  const __bf16* DY;  // [N][H][W][64]
+  float* slab;       // [G][64][576]
+  uint32_t x_bytes;
+  int N, H, W, TR, tiles;
+};
+
+constexpr int HWG_XBUF = 48 * 1024;  // 384 input-image rows x 128 B
+constexpr int HWG_DBUF = 32 * 1024;  // 256 dy rows x 128 B
+
+// transposed (m-major) fragment of a [rows][64] bf16 MTile image: lane l gets
+// column col0 + (l & 15), rows row0 + 8 (l >> 4) .. +7
+__device__ __forceinline__ void read_tfrag(Frag<__bf16>& f, const char* base, int row0, int col0, int lane) {
+  typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = row0 + 8 * g + q;
+  const char* a0 = base + MTile<__bf16, 64>::off(r0, col0 + 4 * p);
+  const char* a1 = base + MTile<__bf16, 64>::off(r0 + 4, col0 + 4 * p);
+  v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a0));
+  v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a1));
+  f.v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArgs a) {
+  typedef __bf16 T;
+  constexpr int NW = 8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (HWG_XBUF + HWG_DBUF)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // k rows 32 wm .. +31; column blocks 9 wn .. 9 wn + 8
+  const int G = gridDim.x, g = blockIdx.x;
+  const int u0 = (int)((long)g * a.tiles / G), u1 = (int)((long)(g + 1) * a.tiles / G);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsD = make_rsrc(a.DY, a.x_bytes);
+  const int Wp = a.W + 2;
+  const int npx = (a.TR + 2) * Wp, mrows = a.TR * Wp;
+
+  auto issue = [&](int tile, char* Xs, char* Ds) {
+    const int R0 = tile * a.TR;
+    const int n = R0 / a.H, p0 = R0 - n * a.H;
+    for (int i = wave; i < HWG_XBUF / 1024; i += NW) {  // input image: 8 rows per instruction
+      const int px = i * 8 + (lane >> 3);
+      const int sr = px / Wp, sc = px - sr * Wp;
+      const int pin = p0 - 1 + sr, win = sc - 1;
+      const int ch = (lane & 7) ^ ((px & 3) << 1);  // MTile<64>: 16-B chunk k at k ^ 2 (row & 3)
+      const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
+      const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
+      blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
+    }
+    for (int i = wave; i < HWG_DBUF / 1024; i += NW) {  // dy rows of the padded grid
+      const int m = i * 8 + (lane >> 3);
+      const int j = m / Wp, q = m - j * Wp;
+      const int ch = (lane & 7) ^ ((m & 3) << 1);
+      const bool ok = m < mrows && q < a.W;
+      const uint32_t off = (uint32_t)(((((long)n * a.H + p0 + j) * a.W + q) * 64 + ch * 8) * 2);
+      blds16(rsD, ok ? off : SSIP_OOB, Ds + i * 1024);
+    }
+  };
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int b = 0; b < 9; ++b) acc[x][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // column block b of this wave: tap t = (9 wn + b) / 4, channels 16 ((9 wn + b) % 4) ..
+  int toff[9], ccol[9];
+#pragma unroll
+  for (int b = 0; b < 9; ++b) {
+    const int nb = 9 * wn + b, t = nb >> 2;
+    toff[b] = (t / 3) * Wp + (t % 3);
+    ccol[b] = (nb & 3) * 16;
+  }
+
+  if (u0 < u1) issue(u0, smem, smem + HWG_XBUF);
+  bool first = true;
+  for (int u = u0; u < u1; ++u) {
+    char* const Xs = smem + ((u - u0) & 1) * (HWG_XBUF + HWG_DBUF);
+    char* const Ds = Xs + HWG_XBUF;
+    char* const Xn = smem + ((u - u0 + 1) & 1) * (HWG_XBUF + HWG_DBUF);
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    first = false;
+    halo_lds_barrier();
+    if (u + 1 < u1) issue(u + 1, Xn, Xn + HWG_XBUF);
+    Frag<T> fa[2][2], fb[2][9];
+    auto load_step = [&](int ks, Frag<T>(&ra)[2], Frag<T>(&rb)[9]) {
+#pragma unroll
+      for (int x = 0; x < 2; ++x) read_tfrag(ra[x], Ds, 32 * ks, (2 * wm + x) * 16, lane);
+#pragma unroll
+      for (int b = 0; b < 9; ++b) read_tfrag(rb[b], Xs, 32 * ks + toff[b], ccol[b], lane);
+    };
+    load_step(0, fa[0], fb[0]);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks + 1 < 8) load_step(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int b = 0; b < 9; ++b) mma(acc[x][b], fa[ks & 1][x], fb[ks & 1][b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's rows land before the barrier
+  }
+  // this workgroup's partial dW: slab[g][k][(t, c)]
+  float* sl = a.slab + (long)g * 64 * 576;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int b = 0; b < 9; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = (2 * wm + x) * 16 + 4 * (lane >> 4) + e;
+        const int col = (9 * wn + b) * 16 + (lane & 15);
+        sl[(long)k * 576 + col] = acc[x][b][e];
+      }
+}
+
+// ---------------------------------------------------------------------------
 // host-side planning
 // ---------------------------------------------------------------------------
 struct Plan {
@@ -2322,6 +2450,33 @@ static int launch_stem_halo(const ssip_conv_desc* d, const HaloPlan& hp, const v
   return ::ssip::check_launch("conv_stem_halo");
 }
 
+// ---- halo WGRAD (conv_halo_wgrad_kernel): 3x3 / stride 1 / pad 1, C = K = 64, bf16
+static bool halo_wg_plan(const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
+  const char* e = getenv("SSIP_HALO");
+  if (e && e[0] == '0') return false;
+  const char* f = getenv("SSIP_CONV_FORCE");
+  if (f && f[0] == 'w') return false;
+  if (dtype != SSIP_BF16 || !desc_ok(d) || d->R != 3 || d->S != 3 || d->stride != 1 || d->pad != 1 ||
+      d->P != d->H || d->Q != d->W || d->C != 64 || d->K != 64)
+    return false;
+  const int Wp = d->W + 2;
+  if (256 + 2 * Wp + 2 > HWG_XBUF / 128) return false;  // shifted reads stay inside the input image
+  int TR = 0;
+  for (int tr = std::min(d->H, 256 / Wp); tr >= 1; --tr)
+    if (d->H % tr == 0 && (tr + 2) * Wp <= HWG_XBUF / 128) {
+      TR = tr;
+      break;
+    }
+  if (TR == 0 || TR * d->W < 128) return false;
+  if ((long)d->N * d->H * d->W * 64 * 2 >= (1l << 31)) return false;
+  hp.TR = TR;
+  hp.cols = 576;
+  hp.tiles = d->N * d->H / TR;
+  hp.units = hp.tiles;
+  hp.G = std::min(hp.tiles, device_cus());
+  return true;
+}
+
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
                        void* out, const void* add, float* partial, hipStream_t st) {
   HaloArgs h;
@@ -2450,6 +2605,8 @@ int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d) {
   if (plan_conv(MODE_WGRAD, d, 2, p2) == SSIP_OK) b = (int64_t)p2.splits * p2.args.M * p2.args.Ng * 4;
   if (plan_conv(MODE_WGRAD, d, 4, p4) == SSIP_OK)
     b = std::max<int64_t>(b, (int64_t)p4.splits * p4.args.M * p4.args.Ng * 4);
+  HaloPlan hp;
+  if (b >= 0 && halo_wg_plan(d, SSIP_BF16, hp)) b = std::max<int64_t>(b, (int64_t)hp.G * 64 * 576 * 4);
   return b;
 }
 
@@ -2463,6 +2620,31 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   SSIP_REQUIRE(workspace_bytes >= need, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
                (long long)workspace_bytes, (long long)need);
   SSIP_REQUIRE(c_real >= 1 && c_real <= d->C && s_real >= 1 && s_real <= d->S, SSIP_ERR_ARG, "bad c_real/s_real");
+  {
+    HaloPlan hp;
+    if (halo_wg_plan(d, dtype, hp)) {
+      const int64_t hneed = (int64_t)hp.G * 64 * 576 * 4;
+      SSIP_REQUIRE(workspace_bytes >= hneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
+                   (long long)workspace_bytes, (long long)hneed);
+      HaloWgArgs h;
+      h.X = static_cast<const __bf16*>(x);
+      h.DY = static_cast<const __bf16*>(dy);
+      h.slab = static_cast<float*>(workspace);
+      h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 64 * 2);
+      h.N = d->N; h.H = d->H; h.W = d->W; h.TR = hp.TR; h.tiles = hp.tiles;
+      hipStream_t st = (hipStream_t)stream;
+      hipLaunchKernelGGL(conv_halo_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+      rc = ::ssip::check_launch("conv_halo_wgrad");
+      if (rc) return rc;
+      const long total4 = 64L * 576 / 4;
+      int lg = 0;
+      while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
+      const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
+                         hp.G, 64, 576, c_real, 3, s_real, 64, 3, dw_kcrs, accumulate, lg);
+      return ::ssip::check_launch("wgrad_reduce");
+    }
+  }
   pl.args.A = dy; pl.args.B = x; pl.args.out = workspace;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);

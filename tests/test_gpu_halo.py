@@ -123,3 +123,37 @@ def test_halo_partial_tiles_is_workgroup_count(dev, monkeypatch):
     assert tiles * 64 * 3 <= ops.conv_fwd_partial_floats(g)
     monkeypatch.setenv("SSIP_HALO", "0")
     assert ops.conv_fwd_partial_tiles(g, torch.bfloat16) == -(-256 * 56 * 56 // 128)
+
+
+@pytest.mark.parametrize("shape", [(2, 56, 56), (3, 16, 16), (5, 56, 56)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_halo_wgrad(dev, shape, accumulate, monkeypatch):
+    """conv_halo_wgrad_kernel (C = K = 64, 3x3/s1/p1): fp32 dW against torch
+    float64 on the bf16 operands (rel-err <= 1e-4, the implicit-GEMM path's
+    bound) and against that path itself (the k-order differs: not bitwise)."""
+    torch.manual_seed(12)
+    N, H, W = shape
+    C = K = 64
+    dt = torch.bfloat16
+    g = ConvGeom(N, H, W, C, K, 3, 3, 1, 1, C, 3)
+    x = torch.randn(N, C, H, W).bfloat16().float()
+    dy = torch.randn(N, K, H, W).bfloat16().float()
+    ref = torch.nn.grad.conv2d_weight(x.double(), (K, C, 3, 3), dy.double(), padding=1)
+    xh = ops.nchw_to_nhwc(x.to(dev), C, dt)
+    dyh = ops.nchw_to_nhwc(dy.to(dev), K, dt)
+    ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
+    base = torch.randn(K, C, 3, 3, device=dev)
+
+    def run():
+        dw = base.clone()
+        ops.conv_wgrad(g, dyh, xh, dw, accumulate, ws)
+        torch.cuda.synchronize()
+        return dw.cpu().double()
+
+    monkeypatch.delenv("SSIP_HALO", raising=False)
+    dw = run()
+    monkeypatch.setenv("SSIP_HALO", "0")
+    dw0 = run()
+    want = ref + (base.cpu().double() if accumulate else 0)
+    assert _relerr(dw, want) < 1e-4
+    assert _relerr(dw, dw0) < 1e-5

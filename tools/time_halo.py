@@ -60,3 +60,16 @@ for N in (256, 128):
         t = time_fn(lambda: ops.conv_fwd(g, x, w, y, part), 20)
         print(f"stem N={N} {'halo' if halo == '1' else 'gemm'} {t:8.1f} us {g.flops() / t / 1e6:7.0f} TF/s", flush=True)
 os.environ["SSIP_HALO"] = "1"
+
+# layer1 wgrad: conv_halo_wgrad_kernel vs the implicit-GEMM split-K path (incl. the slab reduce)
+for N in (256,):
+    g = ops.ConvGeom(N, 56, 56, 64, 64, 3, 3, 1, 1, 64, 3)
+    x = torch.randn(N, 56, 56, 64, device=dev).to(bf)
+    dy = torch.randn(N, 56, 56, 64, device=dev).to(bf)
+    dw = torch.empty(64, 64, 3, 3, device=dev)
+    ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
+    for halo in ("1", "0"):
+        os.environ["SSIP_HALO"] = halo
+        t = time_fn(lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), 20)
+        print(f"wgrad N={N} {'halo' if halo == '1' else 'gemm'} {t:8.1f} us {g.flops() / t / 1e6:7.0f} TF/s", flush=True)
+os.environ["SSIP_HALO"] = "1"

@@ -110,9 +110,13 @@ def main():
     timer = ops.ConvTimer()
     ops.set_conv_timer(timer)
     graph, step.graph = step.graph, False  # the same kernels launched one by one, each bracketed by events
-    side, resnet_mod.WGRAD_SIDE_STREAM = resnet_mod.WGRAD_SIDE_STREAM, False  # wgrads timed without overlap
+    # every launch on one stream: an event bracket must not include queueing
+    # behind a kernel of another stream (weak forward, side-stream wgrads)
+    side, resnet_mod.WGRAD_SIDE_STREAM = resnet_mod.WGRAD_SIDE_STREAM, False
+    overlap, step.overlap = step.overlap, False
     step(x_l, y_l, x_u)
     step.graph = graph
+    step.overlap = overlap
     resnet_mod.WGRAD_SIDE_STREAM = side
     ops.set_conv_timer(None)
     summ = timer.summary()
@@ -169,7 +173,7 @@ def main():
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_note": "bytes per step for the same conv family, PMC FETCH_SIZE*2 + WRITE_SIZE "
                                          "(profiles/r1_pmc_traffic.json; Infinity-Cache hits are counted)",
-                         "kernel": "conv_glds_kernel + conv_gemm_kernel (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
+                         "kernel": "conv family: conv_glds / conv_halo / conv_stem_halo / conv_halo_wgrad (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
                                    f"in {conv_ms:.3f} ms"},
             "cpu_baseline": cpu,

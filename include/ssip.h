@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 2
+#define SSIP_ABI_VERSION 3
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -135,12 +135,16 @@ int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out,
  * ssip_maxpool_fwd).  Backward: dy = BN-backward of the ReLU-masked gathered
  * pool gradient (replaces ssip_maxpool_bwd + ssip_bn_bwd); y is the pre-BN
  * conv output [N][H][W][C]; partial sized by ..._partial_floats; coef 3*C.
+ * ymax (nullable, pooled shape): the forward stores each window's pre-BN
+ * argmax value there, and the backward then reduces over the pooled grid
+ * (dpool + ymax) instead of gathering the full-resolution map twice.
  * ---------------------------------------------------------------------- */
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
-                          const float* scale, const float* shift, void* out, uint8_t* idx, void* stream);
+                          const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream);
 int64_t ssip_stem_pool_bn_bwd_partial_floats(int N, int H, int W, int C);
 int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* dpool,
-                          const uint8_t* idx, const void* y, const float* mean, const float* invstd,
+                          const uint8_t* idx, const void* y, const void* ymax, const float* mean,
+                          const float* invstd,
                           const float* scale, const float* shift, const float* gamma, float* dgamma, float* dbeta,
                           int accumulate, void* dy, float* partial, float* coef, void* stream);
 

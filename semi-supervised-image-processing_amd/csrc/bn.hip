@@ -130,92 +130,6 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const 
   }
 }
 
-// per-(row block, channel) sums of dout and dout*xhat.
-// Block: 256 threads; each thread owns an 8-channel chunk; threads/row = C/8.
-template <typename T>
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T* __restrict__ dz,
-                                     const T* __restrict__ zmask, const T* __restrict__ y,
-                                     const float* __restrict__ mean, const float* __restrict__ invstd,
-                                     const float* __restrict__ mscale, const float* __restrict__ mshift,
-                                     float* __restrict__ partial) {
-  const int cpr = C / 8;               // chunks per row
-  const int rpi = 256 / cpr;           // rows per iteration (>= 1 since C <= 2048)
-  const int chunk = threadIdx.x % cpr;
-  const int rsub = threadIdx.x / cpr;
-  const int c0 = chunk * 8;
-  const long r0 = (long)blockIdx.x * rows_per_block;
-  long r1 = r0 + rows_per_block;
-  if (r1 > M) r1 = M;
-  float sd[8], sx[8], mu[8], is[8], msc[8], msh[8];
-  const bool amask = mscale != nullptr;  // ReLU mask recomputed from y (no z read)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { sd[j] = 0.f; sx[j] = 0.f; msc[j] = 0.f; msh[j] = 0.f; }
-  load_f8(mu, mean + c0);
-  load_f8(is, invstd + c0);
-  if (amask) {
-    load_f8(msc, mscale + c0);
-    load_f8(msh, mshift + c0);
-  }
-  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& yy) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float d = g.get(j);
-      if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
-      if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
-      const float xh = (yy.get(j) - mu[j]) * is[j];
-      sd[j] += d;
-      sx[j] += d * xh;
-    }
-  };
-  if (rsub < rpi) {
-    // two rows in flight per thread; rows accumulate in the same order as a
-    // plain r += rpi walk, so the sums do not depend on the unroll
-    long r = r0 + rsub;
-    for (; r + rpi < r1; r += 2 * rpi) {
-      Vec8<T> g0, g1, z0, z1, y0, y1;
-      g0.load(dz + r * C + c0);
-      g1.load(dz + (r + rpi) * C + c0);
-      y0.load(y + r * C + c0);
-      y1.load(y + (r + rpi) * C + c0);
-      if (zmask) {
-        z0.load(zmask + r * C + c0);
-        z1.load(zmask + (r + rpi) * C + c0);
-      }
-      acc(g0, z0, y0);
-      acc(g1, z1, y1);
-    }
-    if (r < r1) {
-      Vec8<T> g0, z0, y0;
-      g0.load(dz + r * C + c0);
-      y0.load(y + r * C + c0);
-      if (zmask) z0.load(zmask + r * C + c0);
-      acc(g0, z0, y0);
-    }
-  }
-  __shared__ float red[2][256][9];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    red[0][threadIdx.x][j] = sd[j];
-    red[1][threadIdx.x][j] = sx[j];
-  }
-  __syncthreads();
-  // threads with rsub == 0 sum over rsub in fixed order
-  if (threadIdx.x < cpr) {
-    // [C][blocks][2]: each channel's records contiguous for the finalize
-    float* out = partial + ((long)c0 * gridDim.x + blockIdx.x) * 2;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float a = 0.f, b = 0.f;
-      for (int s = 0; s < rpi; ++s) {
-        a += red[0][s * cpr + threadIdx.x][j];
-        b += red[1][s * cpr + threadIdx.x][j];
-      }
-      out[(long)j * gridDim.x * 2] = a;
-      out[(long)j * gridDim.x * 2 + 1] = b;
-    }
-  }
-}
-
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz,
                                                            const T* __restrict__ zmask, const T* __restrict__ y,
@@ -300,15 +214,6 @@ static int bn_elem_grid(long total8) {
   return (int)b;
 }
 
-static int bwd_rows_per_block(long M, int C) {
-  // aim for ~2048 blocks (8 per CU), at least four full iterations of rows
-  const int rpi = 256 / (C / 8);
-  long rows = (M + 2047) / 2048;
-  if (rows < 4 * rpi) rows = 4 * rpi;
-  if (rows < rpi) rows = rpi;
-  rows = ((rows + rpi - 1) / rpi) * rpi;
-  return (int)rows;
-}
 
 }  // namespace
 

@@ -30,7 +30,7 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
                                                                int pad, const T* __restrict__ y,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, T* __restrict__ out,
-                                                               uint8_t* __restrict__ idx) {
+                                                               uint8_t* __restrict__ idx, T* __restrict__ ymax) {
   const int cpr = C >> 3;
   const int row = blockIdx.x;  // n * P + p
   const int n = row / P, p = row - (row / P) * P;
@@ -54,38 +54,40 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
           ok[r * 3 + u] = h >= 0 && h < H && w >= 0 && w < W;
           v[r * 3 + u].load(yb + (ok[r * 3 + u] ? (h * W + w) * C : 0));
         }
-      float best[8];
+      float best[8], ysel[8];
       int bi[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = -1; }
+      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = -1; ysel[j] = 0.f; }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         if (!ok[t]) continue;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float f = to_f32(from_f32<T>(bn_relu(v[t].get(j), sc[j], sh[j])));
-          if (bi[j] < 0 || f > best[j] || f != f) { best[j] = f; bi[j] = t; }
+          if (bi[j] < 0 || f > best[j] || f != f) { best[j] = f; bi[j] = t; ysel[j] = v[t].get(j); }
         }
       }
-      Vec8<T> o;
+      Vec8<T> o, ym;
       uint64_t packed = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         o.set(j, best[j]);
+        ym.set(j, ysel[j]);
         packed |= (uint64_t)(uint8_t)bi[j] << (8 * j);
       }
       const long oi = ((long)row * Q + q) * C + cc * 8;
       o.store(out + oi);
       *reinterpret_cast<uint64_t*>(idx + oi) = packed;
+      if (ymax) ym.store(ymax + oi);
     }
     return;
   }
   for (int e = threadIdx.x; e < Q * cpr; e += blockDim.x) {
     const int q = e / cpr;
-    float best[8];
+    float best[8], ysel[8];
     int bi[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = -1; }
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = -1; ysel[j] = 0.f; }
     for (int r = 0; r < k; ++r) {
       const int h = p * s - pad + r;
       if (h < 0 || h >= H) continue;
@@ -98,20 +100,22 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
         for (int j = 0; j < 8; ++j) {
           // the value ssip_bn_apply would have stored
           const float f = to_f32(from_f32<T>(bn_relu(v.get(j), sc[j], sh[j])));
-          if (bi[j] < 0 || f > best[j] || f != f) { best[j] = f; bi[j] = r * k + u; }
+          if (bi[j] < 0 || f > best[j] || f != f) { best[j] = f; bi[j] = r * k + u; ysel[j] = v.get(j); }
         }
       }
     }
-    Vec8<T> o;
+    Vec8<T> o, ym;
     uint64_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       o.set(j, best[j]);
+      ym.set(j, ysel[j]);
       packed |= (uint64_t)(uint8_t)bi[j] << (8 * j);
     }
     const long oi = ((long)row * Q + q) * C + cc * 8;
     o.store(out + oi);
     *reinterpret_cast<uint64_t*>(idx + oi) = packed;
+    if (ymax) ym.store(ymax + oi);
   }
 }
 
@@ -296,7 +300,7 @@ static int rows_per_block(int N, int H) {
 extern "C" {
 
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
-                          const float* scale, const float* shift, void* out, uint8_t* idx, void* stream) {
+                          const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream) {
   SSIP_REQUIRE(N > 0 && H > 0 && W > 0 && C % 8 == 0 && 256 % (C / 8) == 0 && k > 0 && k * k <= 255 && s > 0 &&
                    y && scale && shift && out && idx,
                SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: bad arguments");
@@ -304,7 +308,7 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
   SSIP_REQUIRE((long)N * H * W * C < (1l << 31), SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: too large");
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(stem_bn_pool_fwd_kernel<T>, dim3(N * P), dim3(256), 0, (hipStream_t)stream, H, W, C, P, Q,
-                       k, s, pad, (const T*)y, scale, shift, (T*)out, idx);
+                       k, s, pad, (const T*)y, scale, shift, (T*)out, idx, (T*)ymax);
   });
   return ::ssip::check_launch("stem_bn_pool_fwd");
 }
@@ -312,11 +316,15 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
 int64_t ssip_stem_pool_bn_bwd_partial_floats(int N, int H, int W, int C) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || 256 % (C / 8)) return -1;
   const int rows = rows_per_block(N, H);
-  return (int64_t)((N * H + rows - 1) / rows) * C * 2;
+  const int64_t full = (int64_t)((N * H + rows - 1) / rows) * C * 2;
+  // the pooled-grid reduction (ymax given): any pooled size <= the full-resolution one
+  const long Mp = (long)N * H * W;
+  const int prow = bwd_rows_per_block(Mp, C);
+  return std::max<int64_t>(full, (int64_t)((Mp + prow - 1) / prow) * C * 2);
 }
 
 int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* dpool,
-                          const uint8_t* idx, const void* y, const float* mean, const float* invstd,
+                          const uint8_t* idx, const void* y, const void* ymax, const float* mean, const float* invstd,
                           const float* scale, const float* shift, const float* gamma, float* dgamma, float* dbeta,
                           int accumulate, void* dy, float* partial, float* coef, void* stream) {
   SSIP_REQUIRE(N > 0 && H > 0 && W > 0 && C % 8 == 0 && 128 % (C / 8) == 0 && k > 0 && k * k <= 255 && s > 0 &&
@@ -328,10 +336,22 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   hipStream_t st = (hipStream_t)stream;
   const int rows = rows_per_block(N, H);
   const int blocks = (N * H + rows - 1) / rows;
+  // with ymax (the pre-BN value at each window's argmax, from the forward)
+  // the sums run over the pooled grid: every full-resolution pixel's masked
+  // gradient is the sum of the pooled gradients of the windows that chose it,
+  // so sum d = sum_windows mask(ymax) dpool and likewise for d * xhat
+  const long Mp = (long)N * P * Q;
+  const int prow = ymax ? bwd_rows_per_block(Mp, C) : 0;
+  const int red_blocks = ymax ? (int)((Mp + prow - 1) / prow) : blocks;
+  SSIP_REQUIRE(!ymax || 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_stem_pool_bn_bwd: unsupported C");
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
-                       pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, M, 1, partial, gamma, mean,
+    if (ymax)
+      hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(red_blocks), dim3(256), 0, st, Mp, C, prow, (const T*)dpool,
+                         (const T*)nullptr, (const T*)ymax, mean, invstd, scale, shift, partial);
+    else
+      hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
+                         pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, red_blocks, M, 1, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
                        (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);

@@ -79,9 +79,9 @@ _SIGS = {
     "ssip_bn_relu_bwd": (_c_int, [_c_int, _c_i64, _c_int] + [_vp] * 9 + [_c_int, _vp, _vp, _vp, _vp]),
     "ssip_bn_bwd_from_partials": (_c_int, [_c_int, _c_i64, _c_int, _c_int] + [_vp] * 8 + [_c_int, _vp, _vp, _vp]),
     "ssip_relu_bwd": (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp]),
-    "ssip_stem_bn_pool_fwd": (_c_int, [_c_int] * 8 + [_vp] * 6),
+    "ssip_stem_bn_pool_fwd": (_c_int, [_c_int] * 8 + [_vp] * 7),
     "ssip_stem_pool_bn_bwd_partial_floats": (_c_i64, [_c_int] * 4),
-    "ssip_stem_pool_bn_bwd": (_c_int, [_c_int] * 8 + [_vp] * 10 + [_c_int] + [_vp] * 4),
+    "ssip_stem_pool_bn_bwd": (_c_int, [_c_int] * 8 + [_vp] * 11 + [_c_int] + [_vp] * 4),
     "ssip_maxpool_fwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),
     "ssip_maxpool_bwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),
     "ssip_avgpool_fc_fwd": (_c_int, [_c_int] * 5 + [_vp] * 6),

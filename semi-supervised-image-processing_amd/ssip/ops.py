@@ -263,10 +263,11 @@ def bn_bwd_from_partials(M: int, C: int, tiles: int, partial, dout, y, mean, inv
          _p(invstd), _p(gamma), _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(coef), stream_ptr())
 
 
-def stem_bn_pool_fwd(N, H, W, C, k, s, pad, y, scale, shift, out, idx) -> None:
-    """maxpool(relu(BN(y))) with argmax bytes, no full-resolution activation."""
+def stem_bn_pool_fwd(N, H, W, C, k, s, pad, y, scale, shift, out, idx, ymax=None) -> None:
+    """maxpool(relu(BN(y))) with argmax bytes, no full-resolution activation;
+    ymax (optional, pooled shape): y at each window's argmax, for the backward."""
     call("ssip_stem_bn_pool_fwd", dtype_code(y), N, H, W, C, k, s, pad, _p(y), _p(scale), _p(shift), _p(out),
-         _p(idx), stream_ptr())
+         _p(idx), _p(ymax), stream_ptr())
 
 
 def stem_pool_bn_bwd_partial_floats(N, H, W, C) -> int:
@@ -274,10 +275,11 @@ def stem_pool_bn_bwd_partial_floats(N, H, W, C) -> int:
 
 
 def stem_pool_bn_bwd(N, H, W, C, k, s, pad, dpool, idx, y, mean, invstd, scale, shift, gamma, dgamma, dbeta,
-                     accumulate: bool, dy, partial, coef) -> None:
+                     accumulate: bool, dy, partial, coef, ymax=None) -> None:
     """BN(+ReLU) backward of the stem through the max-pool, one reduction pass
-    and one apply pass over y (see include/ssip.h)."""
-    call("ssip_stem_pool_bn_bwd", dtype_code(y), N, H, W, C, k, s, pad, _p(dpool), _p(idx), _p(y), _p(mean),
+    (over the pooled grid when the forward's ymax is given) and one apply pass
+    over y (see include/ssip.h)."""
+    call("ssip_stem_pool_bn_bwd", dtype_code(y), N, H, W, C, k, s, pad, _p(dpool), _p(idx), _p(y), _p(ymax), _p(mean),
          _p(invstd), _p(scale), _p(shift), _p(gamma), _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(partial),
          _p(coef), stream_ptr())
 

@@ -158,6 +158,7 @@ class _Saved:
     stem: _ConvRec = None
     pool_out: torch.Tensor = None
     pool_idx: torch.Tensor = None
+    pool_ymax: torch.Tensor = None  # pre-BN y at each max-pool window's argmax (stem backward)
     pool_hw: Tuple[int, int] = (0, 0)
     blocks: List[Tuple[List[_ConvRec], Optional[_ConvRec], torch.Tensor]] = field(default_factory=list)
     feat: torch.Tensor = None
@@ -385,9 +386,11 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
     pool = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt)
     idx = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=torch.uint8)
     # BN -> ReLU -> max-pool in one pass over y (the full-resolution z is never stored)
-    ops.stem_bn_pool_fwd(N, g.P, g.Q, g.K, k, s, pd, rec.y, rec.stats[2], rec.stats[3], pool, idx)
+    ymax = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt) if save else None
+    ops.stem_bn_pool_fwd(N, g.P, g.Q, g.K, k, s, pd, rec.y, rec.stats[2], rec.stats[3], pool, idx, ymax)
     if save:
         sv.stem, sv.pool_out, sv.pool_idx, sv.pool_hw = rec, pool, idx, (g.P, g.Q)
+        sv.pool_ymax = ymax
     x, Hc, Wc = pool, Hp, Wp
     for blk in model.blocks():
         recs = []
@@ -685,7 +688,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     partial = torch.empty(ops.stem_pool_bn_bwd_partial_floats(N, P1, Q1, C1), device=dev, dtype=torch.float32)
     ops.stem_pool_bn_bwd(N, P1, Q1, C1, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, stem.y,
                          stem.stats[0], stem.stats[1], stem.stats[2], stem.stats[3], stem.bn.weight.detach(), dgam,
-                         dbet, acc, dy1, partial, coef_buf[: 3 * C1])
+                         dbet, acc, dy1, partial, coef_buf[: 3 * C1], sv.pool_ymax)
     conv_wgrad(stem, dy1)
     if hook is not None:
         hook([model.conv1.weight, model.bn1.weight, model.bn1.bias])

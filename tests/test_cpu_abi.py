@@ -18,7 +18,7 @@ def test_library_exports_every_symbol():
     lib = _lib.lib()
     for name in _lib.EXPORTED_SYMBOLS:
         assert hasattr(lib, name), name
-    assert lib.ssip_version() == 2
+    assert lib.ssip_version() == 3
 
 
 def test_argument_errors_surface_as_status_codes():

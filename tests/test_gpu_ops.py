@@ -284,10 +284,17 @@ def test_stem_bn_pool_fused_matches_unfused(dev, dtname):
     # fused
     pool = torch.empty_like(pool_r)
     idx = torch.empty_like(idx_r)
-    ops.stem_bn_pool_fwd(N, H, W, C, k, s, pd, y, scale, shift, pool, idx)
+    ymax = torch.empty_like(pool_r)
+    ops.stem_bn_pool_fwd(N, H, W, C, k, s, pd, y, scale, shift, pool, idx, ymax)
     torch.cuda.synchronize()
     assert torch.equal(pool.cpu(), pool_r.cpu())
     assert torch.equal(idx.cpu(), idx_r.cpu())
+    # ymax = y at each window's argmax (torch's first-max order)
+    Hp, Wp = P, Q
+    yp = torch.nn.functional.pad(y.float().permute(0, 3, 1, 2), (pd, pd, pd, pd))
+    win = yp.unfold(2, k, s).unfold(3, k, s)[:, :, :Hp, :Wp].reshape(N, C, Hp, Wp, k * k)
+    want = torch.gather(win, 4, idx.permute(0, 3, 1, 2).long().unsqueeze(-1)).squeeze(-1).permute(0, 2, 3, 1)
+    assert torch.equal(ymax.float().cpu(), want.cpu())
     # backward
     dpool = torch.randn(N, P, Q, C, device=dev).to(dt)
     dz = torch.empty_like(y)
@@ -303,13 +310,14 @@ def test_stem_bn_pool_fused_matches_unfused(dev, dtname):
     db = torch.empty(C, device=dev)
     part2 = torch.empty(ops.stem_pool_bn_bwd_partial_floats(N, H, W, C), device=dev)
     coef2 = torch.empty(3 * C, device=dev)
-    ops.stem_pool_bn_bwd(N, H, W, C, k, s, pd, dpool, idx, y, mean, invstd, scale, shift, gamma, dg, db, False, dy,
-                         part2, coef2)
-    torch.cuda.synchronize()
     tol = 1e-5 if dt == torch.float32 else 2e-2
-    assert _rel(dy, dy_r) < tol
-    assert _rel(dg, dg_r) < tol
-    assert _rel(db, db_r) < tol
+    for ym in (None, ymax):  # full-resolution gather reduction / pooled-grid reduction
+        ops.stem_pool_bn_bwd(N, H, W, C, k, s, pd, dpool, idx, y, mean, invstd, scale, shift, gamma, dg, db, False,
+                             dy, part2, coef2, ym)
+        torch.cuda.synchronize()
+        assert _rel(dy, dy_r) < tol
+        assert _rel(dg, dg_r) < tol
+        assert _rel(db, db_r) < tol
 
 
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])

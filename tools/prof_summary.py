@@ -14,6 +14,12 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 
 
 def family(n):
+    if "conv_halo_wgrad_kernel" in n:
+        return "conv_wgrad"
+    if "conv_stem_halo_kernel" in n:
+        return "conv_fwd"
+    if "conv_halo_kernel" in n:
+        return "conv_halo (layer1 fwd + dgrad)"
     for key in ("conv_gemm_kernel<", "conv_glds_kernel<"):
         if key in n:
             mode = n.split(key)[1][0]

@@ -5,7 +5,7 @@
 # and tools/pmc_traffic.py, then copy the summaries into profiles/.
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/prof_r1
+out=gpurun_out/prof_r1b
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
   python bench.py --steps 10 --warmup 5 --no-cpu-baseline > $out/trace.log 2>&1 || { tail -20 $out/trace.log; exit 1; }

@@ -2037,6 +2037,125 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
 }
 
 // ---------------------------------------------------------------------------
+// WGRAD of the stem conv (7x7 / stride 2 over the pre-padded NHWC4 image):
+//   dW[k][(r, s, c)] = sum_m dy[m][k] * x[2p + r][2q + s][c]
+// Per tile of STEM_TR output rows (GEMM rows m = j * QP + q, dy zero for
+// q >= Q) a persistent workgroup stages the 9 contiguous input rows (as
+// conv_stem_halo_kernel) and the tile's dy rows (m-major MTile image), both
+// double-buffered, and keeps the 64 x 224 fp32 result in registers across
+// its tiles.  The x operand of column block (r, 16 of the 32 (s, c)) for
+// row m is the 64-B run at input row 2j + r, pixel 2q: transposed fragment
+// reads with per-lane row addresses (overlapping runs).  One fp32 slab per
+// workgroup, summed by wgrad_reduce_kernel.
+// ---------------------------------------------------------------------------
+struct StemWgArgs {
+  const __bf16* X;   // [N][H][W][4]
+  const __bf16* DY;  // [N][P][Q][64]
+  float* slab;       // [G][64][224]
+  uint32_t x_bytes, dy_bytes;
+  int N, H, W, P, Q, tiles;
+};
+
+constexpr int SWG_DBUF = 32 * 1024;  // 256 dy rows x 128 B
+
+__global__ void __launch_bounds__(512, 2) conv_stem_wgrad_kernel(const StemWgArgs a) {
+  typedef __bf16 T;
+  typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
+  constexpr int NW = 8, NB = 14;  // 224 / 16 column blocks
+  __shared__ __attribute__((aligned(16))) char smem[2 * (STEM_XBUF + SWG_DBUF)];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // k rows 32 wm .. +31; column blocks wn, wn + 4, ...
+  const int G = gridDim.x, g = blockIdx.x;
+  const int u0 = (int)((long)g * a.tiles / G), u1 = (int)((long)(g + 1) * a.tiles / G);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsD = make_rsrc(a.DY, a.dy_bytes);
+  const int xpitch = a.W * 8;
+  const int xrun = STEM_XROWS * xpitch;
+  const int nxi = (xrun + 1023) >> 10;
+
+  auto issue = [&](int tile, char* Xs, char* Ds) {
+    const int R0 = tile * STEM_TR;
+    const int n = R0 / a.P, p0 = R0 - n * a.P;
+    const uint32_t xbase = (uint32_t)((((long)n * a.H + 2 * p0) * a.W) * 8);
+    for (int i = wave; i < nxi; i += NW) {
+      const int b = i * 1024 + lane * 16;
+      blds16(rsX, b < xrun ? xbase + (uint32_t)b : SSIP_OOB, Xs + i * 1024);
+    }
+    for (int i = wave; i < SWG_DBUF / 1024; i += NW) {
+      const int m = i * 8 + (lane >> 3);
+      const int j = m / STEM_QP, q = m - j * STEM_QP;
+      const int ch = (lane & 7) ^ ((m & 3) << 1);  // MTile<64> swizzle
+      const bool ok = q < a.Q;
+      const uint32_t off = (uint32_t)(((((long)n * a.P + p0 + j) * a.Q + q) * 64 + ch * 8) * 2);
+      blds16(rsD, ok ? off : SSIP_OOB, Ds + i * 1024);
+    }
+  };
+
+  const int nbw = wn < NB - 12 ? 4 : 3;  // column blocks of this wave: wn + 4 b, b < nbw
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[x][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // x fragment addressing: lane (g, q, p) reads rows m = row0 + 8 g + q (+4),
+  // columns 4p .. 4p+3 of its block; row m's run starts at (2j + r) xpitch + 16 q_m
+  const int lg = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+
+  if (u0 < u1) issue(u0, smem, smem + STEM_XBUF);
+  bool first = true;
+  for (int u = u0; u < u1; ++u) {
+    char* const Xs = smem + ((u - u0) & 1) * (STEM_XBUF + SWG_DBUF);
+    char* const Ds = Xs + STEM_XBUF;
+    char* const Xn = smem + ((u - u0 + 1) & 1) * (STEM_XBUF + SWG_DBUF);
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    first = false;
+    halo_lds_barrier();
+    if (u + 1 < u1) issue(u + 1, Xn, Xn + STEM_XBUF);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      Frag<T> fa[2], fb[4];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) read_tfrag(fa[x], Ds, 32 * ks, (2 * wm + x) * 16, lane);
+      // the lane's two rows (lo: +0, hi: +4) of this k-step
+      const int m_lo = 32 * ks + 8 * lg + lq, m_hi = m_lo + 4;
+      const int jl = m_lo / STEM_QP, ql = m_lo - jl * STEM_QP;
+      const int jh = m_hi / STEM_QP, qh = m_hi - jh * STEM_QP;
+      const int base_lo = 2 * jl * xpitch + (ql < a.Q ? ql : 0) * 16;  // rows past Q meet dy = 0
+      const int base_hi = 2 * jh * xpitch + (qh < a.Q ? qh : 0) * 16;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (b < nbw) {
+          const int nb = wn + 4 * b, r = nb >> 1, cofs = ((nb & 1) * 16 + 4 * lp) * 2;
+          const char* a0 = Xs + base_lo + r * xpitch + cofs;
+          const char* a1 = Xs + base_hi + r * xpitch + cofs;
+          v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a0));
+          v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a1));
+          fb[b].v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (b < nbw) mma(acc[x][b], fa[x], fb[b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  float* sl = a.slab + (long)g * 64 * 224;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < nbw)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = (2 * wm + x) * 16 + 4 * (lane >> 4) + e;
+          const int col = (wn + 4 * b) * 16 + (lane & 15);
+          sl[(long)k * 224 + col] = acc[x][b][e];
+        }
+}
+
+// ---------------------------------------------------------------------------
 // host-side planning
 // ---------------------------------------------------------------------------
 struct Plan {
@@ -2477,6 +2596,18 @@ static bool halo_wg_plan(const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
   return true;
 }
 
+// ---- stem WGRAD (conv_stem_wgrad_kernel)
+static bool stem_wg_plan(const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
+  const char* e = getenv("SSIP_HALO");
+  if (e && e[0] == '0') return false;
+  const char* f = getenv("SSIP_CONV_FORCE");
+  if (f && f[0] == 'w') return false;
+  if (!stem_plan(d, dtype, hp) || d->K != 64) return false;  // same geometry as the forward's kernel
+  hp.G = std::min(hp.tiles, device_cus());
+  hp.units = hp.tiles;
+  return true;
+}
+
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
                        void* out, const void* add, float* partial, hipStream_t st) {
   HaloArgs h;
@@ -2607,6 +2738,7 @@ int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d) {
     b = std::max<int64_t>(b, (int64_t)p4.splits * p4.args.M * p4.args.Ng * 4);
   HaloPlan hp;
   if (b >= 0 && halo_wg_plan(d, SSIP_BF16, hp)) b = std::max<int64_t>(b, (int64_t)hp.G * 64 * 576 * 4);
+  if (b >= 0 && stem_wg_plan(d, SSIP_BF16, hp)) b = std::max<int64_t>(b, (int64_t)hp.G * 64 * 224 * 4);
   return b;
 }
 
@@ -2622,6 +2754,29 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   SSIP_REQUIRE(c_real >= 1 && c_real <= d->C && s_real >= 1 && s_real <= d->S, SSIP_ERR_ARG, "bad c_real/s_real");
   {
     HaloPlan hp;
+    if (stem_wg_plan(d, dtype, hp)) {
+      const int64_t sneed = (int64_t)hp.G * 64 * 224 * 4;
+      SSIP_REQUIRE(workspace_bytes >= sneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
+                   (long long)workspace_bytes, (long long)sneed);
+      StemWgArgs h;
+      h.X = static_cast<const __bf16*>(x);
+      h.DY = static_cast<const __bf16*>(dy);
+      h.slab = static_cast<float*>(workspace);
+      h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 8);
+      h.dy_bytes = (uint32_t)((long)d->N * d->P * d->Q * 64 * 2);
+      h.N = d->N; h.H = d->H; h.W = d->W; h.P = d->P; h.Q = d->Q; h.tiles = hp.tiles;
+      hipStream_t st = (hipStream_t)stream;
+      hipLaunchKernelGGL(conv_stem_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+      rc = ::ssip::check_launch("conv_stem_wgrad");
+      if (rc) return rc;
+      const long total4 = 64L * 224 / 4;
+      int lg = 0;
+      while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
+      const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
+                         hp.G, 64, 224, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
+      return ::ssip::check_launch("wgrad_reduce");
+    }
     if (halo_wg_plan(d, dtype, hp)) {
       const int64_t hneed = (int64_t)hp.G * 64 * 576 * 4;
       SSIP_REQUIRE(workspace_bytes >= hneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",

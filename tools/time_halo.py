@@ -73,3 +73,15 @@ for N in (256,):
         t = time_fn(lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), 20)
         print(f"wgrad N={N} {'halo' if halo == '1' else 'gemm'} {t:8.1f} us {g.flops() / t / 1e6:7.0f} TF/s", flush=True)
 os.environ["SSIP_HALO"] = "1"
+
+# stem wgrad: conv_stem_wgrad_kernel vs the implicit-GEMM split-K path (incl. the slab reduce)
+g = ops.ConvGeom(256, 230, 230, 4, 64, 7, 8, 2, 0, 3, 7)
+x = torch.randn(256, 230, 230, 4, device=dev).to(bf)
+dy = torch.randn(256, 112, 112, 64, device=dev).to(bf)
+dw = torch.empty(64, 3, 7, 7, device=dev)
+ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
+for halo in ("1", "0"):
+    os.environ["SSIP_HALO"] = halo
+    t = time_fn(lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), 10)
+    print(f"stem wgrad {'halo' if halo == '1' else 'gemm'} {t:8.1f} us {g.flops() / t / 1e6:7.0f} TF/s", flush=True)
+os.environ["SSIP_HALO"] = "1"

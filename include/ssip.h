@@ -134,7 +134,8 @@ int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out,
  * the full-resolution activation (bit-identical to ssip_bn_apply followed by
  * ssip_maxpool_fwd).  Backward: dy = BN-backward of the ReLU-masked gathered
  * pool gradient (replaces ssip_maxpool_bwd + ssip_bn_bwd); y is the pre-BN
- * conv output [N][H][W][C]; partial sized by ..._partial_floats; coef 3*C.
+ * conv output [N][H][W][C]; partial sized by ..._partial_floats; coef 3*C;
+ * dy may be NULL (dgamma / dbeta / coef only: see ssip_stem_bwd_wgrad).
  * ymax (nullable, pooled shape): the forward stores each window's pre-BN
  * argmax value there, and the backward then reduces over the pooled grid
  * (dpool + ymax) instead of gathering the full-resolution map twice.
@@ -142,6 +143,18 @@ int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out,
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
                           const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream);
 int64_t ssip_stem_pool_bn_bwd_partial_floats(int N, int H, int W, int C);
+/* The stem backward tail fused (bf16, 224x224 input): dW (+)= wgrad of the
+ * stem conv with dy = BN-backward apply of the ReLU-masked, argmax-gathered
+ * pooled gradient, formed per tile in LDS (never written).  coef: the 3*64
+ * apply coefficients from ssip_stem_pool_bn_bwd called with dy = NULL (which
+ * then only produces dgamma / dbeta / coef).  d describes the stem conv
+ * (pre-padded NHWC4 input x); y its pre-BN output; dpool / idx pooled.
+ * Workspace: ssip_conv_wgrad_workspace_bytes(d). */
+int ssip_stem_bwd_wgrad_supported(const ssip_conv_desc* d, int dtype);
+int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, const uint8_t* idx, const void* y,
+                        const void* x, const float* scale, const float* shift, const float* coef, float* dw_kcrs,
+                        int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
+                        void* stream);
 int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* dpool,
                           const uint8_t* idx, const void* y, const void* ymax, const float* mean,
                           const float* invstd,

@@ -2156,6 +2156,194 @@ __global__ void __launch_bounds__(512, 2) conv_stem_wgrad_kernel(const StemWgArg
 }
 
 // ---------------------------------------------------------------------------
+// Stem backward tail fused: the BN(+ReLU, through the 3x3/2/1 max-pool)
+// backward apply pass and the stem wgrad in one persistent kernel, so the
+// full-resolution dy never goes through HBM.  Per tile of 2 conv-output
+// rows (h0 = 2T, 2T+1) a workgroup DMAs (double-buffered) the 9 input rows,
+// the 2 pre-BN rows y, and pooled rows T, T+1 of dpool and the argmax bytes;
+// then forms dy = A*d + B*y + C in LDS (d = the argmax-gathered pooled
+// gradient masked by relu(fma(y, scale, shift)) > 0, exactly as
+// stem_pool_bn_bwd_apply_kernel) as an m-major MTile image over the 224
+// output pixels, and runs conv_stem_wgrad_kernel's MFMA loop on it.
+// ---------------------------------------------------------------------------
+struct StemBwArgs {
+  const __bf16* X;      // [N][H][W][4]   pre-padded image
+  const __bf16* Y;      // [N][P][Q][64]  pre-BN stem conv output
+  const __bf16* DP;     // [N][P2][Q2][64] pooled gradient
+  const uint8_t* IX;    // [N][P2][Q2][64] argmax bytes
+  const float* scale;   // BN affine (ReLU mask)
+  const float* shift;
+  const float* coef;    // [3][64] from the BN-backward finalize
+  float* slab;          // [G][64][224]
+  uint32_t x_bytes, y_bytes, dp_bytes, ix_bytes;
+  int N, H, W, P, Q, P2, Q2, tiles;
+};
+
+constexpr int SBW_Y = 28 * 1024, SBW_DP = 14 * 1024, SBW_IX = 7 * 1024;
+constexpr int SBW_IN = STEM_XBUF + SBW_Y + SBW_DP + SBW_IX;  // one input buffer (66 KiB)
+constexpr int SBW_D = 28 * 1024;                             // dy image: 224 rows x 128 B
+
+__global__ void __launch_bounds__(512, 2) conv_stem_bwd_wgrad_kernel(const StemBwArgs a) {
+  typedef __bf16 T;
+  typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
+  constexpr int NW = 8, NB = 14, MR = 224;  // column blocks; GEMM rows (2 x 112 output pixels)
+  static_assert(2 * SBW_IN + SBW_D <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SBW_IN + SBW_D];
+  char* const Dimg = smem + 2 * SBW_IN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int u0 = (int)((long)g * a.tiles / G), u1 = (int)((long)(g + 1) * a.tiles / G);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsY = make_rsrc(a.Y, a.y_bytes);
+  const __amdgpu_buffer_rsrc_t rsP = make_rsrc(a.DP, a.dp_bytes), rsI = make_rsrc(a.IX, a.ix_bytes);
+  const int xpitch = a.W * 8;
+  const int xrun = STEM_XROWS * xpitch;
+  const int yrun = 2 * a.Q * 128, prow = a.Q2 * 128, irow = a.Q2 * 64;
+
+  auto issue = [&](int tile, char* B) {
+    const int R0 = tile * 2;  // conv-output rows R0, R0+1 of the flattened (n, p) space
+    const int n = R0 / a.P, h0 = R0 - n * a.P, T0 = h0 >> 1;
+    const uint32_t xb = (uint32_t)((((long)n * a.H + 2 * h0) * a.W) * 8);  // input rows 2 h0 .. 2 h0 + 8
+    const uint32_t yb = (uint32_t)((((long)n * a.P + h0) * a.Q) * 128);
+    const int prows = (T0 + 1 < a.P2) ? 2 : 1;
+    const uint32_t pb = (uint32_t)((((long)n * a.P2 + T0) * a.Q2) * 128);
+    const uint32_t ib = (uint32_t)((((long)n * a.P2 + T0) * a.Q2) * 64);
+    for (int i = wave; i < STEM_XBUF / 1024; i += NW) {
+      const int b = i * 1024 + lane * 16;
+      blds16(rsX, b < xrun ? xb + (uint32_t)b : SSIP_OOB, B + i * 1024);
+    }
+    for (int i = wave; i < SBW_Y / 1024; i += NW) {
+      const int b = i * 1024 + lane * 16;
+      blds16(rsY, b < yrun ? yb + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + i * 1024);
+    }
+    for (int i = wave; i < SBW_DP / 1024; i += NW) {
+      const int b = i * 1024 + lane * 16;
+      blds16(rsP, b < prows * prow ? pb + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + SBW_Y + i * 1024);
+    }
+    for (int i = wave; i < SBW_IX / 1024; i += NW) {
+      const int b = i * 1024 + lane * 16;
+      blds16(rsI, b < prows * irow ? ib + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + SBW_Y + SBW_DP + i * 1024);
+    }
+  };
+
+  // this thread's 8-channel chunk in the dy pass is fixed (items id = tid + 512 i)
+  const int cc = tid & 7, c0 = cc * 8;
+  float sc[8], sh[8], ca[8], cb[8], ck[8];
+  load_f8(sc, a.scale + c0);
+  load_f8(sh, a.shift + c0);
+  load_f8(ca, a.coef + c0);
+  load_f8(cb, a.coef + 64 + c0);
+  load_f8(ck, a.coef + 128 + c0);
+
+  const int nbw = wn < NB - 12 ? 4 : 3;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[x][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int lg = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+
+  if (u0 < u1) issue(u0, smem);
+  bool first = true;
+  for (int u = u0; u < u1; ++u) {
+    char* const Bc = smem + ((u - u0) & 1) * SBW_IN;
+    char* const Bn = smem + ((u - u0 + 1) & 1) * SBW_IN;
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    first = false;
+    halo_lds_barrier();  // this tile's inputs landed; the dy image and the other buffer are free
+    if (u + 1 < u1) issue(u + 1, Bn);
+    {
+      // ---- dy for the tile's 224 output pixels, into the m-major MTile image
+      const int R0 = u * 2;
+      const int h0 = R0 - (R0 / a.P) * a.P, T0 = h0 >> 1;
+      const char* Ys = Bc + STEM_XBUF;
+      const char* Ps = Ys + SBW_Y;
+      const char* Is = Ps + SBW_DP;
+      for (int id = tid; id < MR * 8; id += 512) {
+        const int m = id >> 3;
+        const int j = m >= a.Q ? 1 : 0, w = m - j * a.Q, h = h0 + j;
+        // windows (p, q) with 2p-1 <= h <= 2p+1, 2q-1 <= w <= 2q+1 (k 3, s 2, pad 1), p, q ascending
+        float dz[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[e] = 0.f;
+        const int plo = h >> 1, phi = min((h + 1) >> 1, a.P2 - 1);
+        const int qlo = w >> 1, qhi = min((w + 1) >> 1, a.Q2 - 1);
+#pragma unroll
+        for (int pa = 0; pa < 2; ++pa) {
+          const int pp = plo + pa;
+          if (pp > phi) continue;
+          const int pr = pp - T0;  // 0 or 1: the staged pooled row
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+            const int qq = qlo + qb;
+            if (qq > qhi) continue;
+            const int pos = (h - (2 * pp - 1)) * 3 + (w - (2 * qq - 1));
+            const uint64_t pk = *reinterpret_cast<const uint64_t*>(Is + (pr * a.Q2 + qq) * 64 + c0);
+            Vec8<T> gv;
+            gv.v = *reinterpret_cast<const i32x4*>(Ps + (pr * a.Q2 + qq) * 128 + c0 * 2);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if ((int)((pk >> (8 * e)) & 0xff) == pos) dz[e] += gv.get(e);
+          }
+        }
+        Vec8<T> yy, o;
+        yy.v = *reinterpret_cast<const i32x4*>(Ys + (j * a.Q + w) * 128 + c0 * 2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float yv = yy.get(e);
+          const float t = __builtin_fmaf(yv, sc[e], sh[e]);
+          const float d = (t > 0.f ? t : 0.f) > 0.f ? dz[e] : 0.f;
+          o.set(e, ca[e] * d + cb[e] * yv + ck[e]);
+        }
+        *reinterpret_cast<i32x4*>(Dimg + m * 128 + ((cc ^ ((m & 3) << 1)) << 4)) = o.v;
+      }
+    }
+    halo_lds_barrier();  // dy image complete
+    const char* Xs = Bc;
+#pragma unroll
+    for (int ks = 0; ks < MR / 32; ++ks) {
+      Frag<T> fa[2], fb[4];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) read_tfrag(fa[x], Dimg, 32 * ks, (2 * wm + x) * 16, lane);
+      const int m_lo = 32 * ks + 8 * lg + lq, m_hi = m_lo + 4;
+      const int jl = m_lo >= a.Q ? 1 : 0, ql = m_lo - jl * a.Q;
+      const int jh = m_hi >= a.Q ? 1 : 0, qh = m_hi - jh * a.Q;
+      const int base_lo = 2 * jl * xpitch + ql * 16, base_hi = 2 * jh * xpitch + qh * 16;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (b < nbw) {
+          const int nb = wn + 4 * b, r = nb >> 1, cofs = ((nb & 1) * 16 + 4 * lp) * 2;
+          const char* a0 = Xs + base_lo + r * xpitch + cofs;
+          const char* a1 = Xs + base_hi + r * xpitch + cofs;
+          v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a0));
+          v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a1));
+          fb[b].v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (b < nbw) mma(acc[x][b], fa[x], fb[b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  float* sl = a.slab + (long)g * 64 * 224;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (b < nbw)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = (2 * wm + x) * 16 + 4 * (lane >> 4) + e;
+          const int col = (wn + 4 * b) * 16 + (lane & 15);
+          sl[(long)k * 224 + col] = acc[x][b][e];
+        }
+}
+
+// ---------------------------------------------------------------------------
 // host-side planning
 // ---------------------------------------------------------------------------
 struct Plan {
@@ -2823,6 +3011,50 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
                      pl.splits, d->K, pl.args.Ng, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
+  return ::ssip::check_launch("wgrad_reduce");
+}
+
+int ssip_stem_bwd_wgrad_supported(const ssip_conv_desc* d, int dtype) {
+  HaloPlan hp;
+  return (stem_wg_plan(d, dtype, hp) && d->Q * 2 == 224 && d->P % 2 == 0) ? 1 : 0;
+}
+
+int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, const uint8_t* idx, const void* y,
+                        const void* x, const float* scale, const float* shift, const float* coef, float* dw_kcrs,
+                        int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
+                        void* stream) {
+  HaloPlan hp;
+  SSIP_REQUIRE(ssip_stem_bwd_wgrad_supported(d, dtype) && stem_wg_plan(d, dtype, hp), SSIP_ERR_ARG,
+               "ssip_stem_bwd_wgrad: unsupported geometry");
+  SSIP_REQUIRE(dpool && idx && y && x && scale && shift && coef && dw_kcrs && workspace, SSIP_ERR_ARG,
+               "ssip_stem_bwd_wgrad: null pointer");
+  SSIP_REQUIRE(c_real >= 1 && c_real <= d->C && s_real >= 1 && s_real <= d->S, SSIP_ERR_ARG, "bad c_real/s_real");
+  const int64_t need = (int64_t)hp.G * 64 * 224 * 4;
+  SSIP_REQUIRE(workspace_bytes >= need, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
+               (long long)workspace_bytes, (long long)need);
+  const int P2 = (d->P + 2 - 3) / 2 + 1, Q2 = (d->Q + 2 - 3) / 2 + 1;  // the 3x3 / 2 / 1 max-pool
+  StemBwArgs h;
+  h.X = static_cast<const __bf16*>(x);
+  h.Y = static_cast<const __bf16*>(y);
+  h.DP = static_cast<const __bf16*>(dpool);
+  h.IX = idx;
+  h.scale = scale; h.shift = shift; h.coef = coef;
+  h.slab = static_cast<float*>(workspace);
+  h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 8);
+  h.y_bytes = (uint32_t)((long)d->N * d->P * d->Q * 64 * 2);
+  h.dp_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64 * 2);
+  h.ix_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64);
+  h.N = d->N; h.H = d->H; h.W = d->W; h.P = d->P; h.Q = d->Q; h.P2 = P2; h.Q2 = Q2; h.tiles = hp.tiles;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv_stem_bwd_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+  int rc = ::ssip::check_launch("conv_stem_bwd_wgrad");
+  if (rc) return rc;
+  const long total4 = 64L * 224 / 4;
+  int lg = 0;
+  while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
+  const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace, hp.G,
+                     64, 224, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
   return ::ssip::check_launch("wgrad_reduce");
 }
 

@@ -328,7 +328,7 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
                           const float* scale, const float* shift, const float* gamma, float* dgamma, float* dbeta,
                           int accumulate, void* dy, float* partial, float* coef, void* stream) {
   SSIP_REQUIRE(N > 0 && H > 0 && W > 0 && C % 8 == 0 && 128 % (C / 8) == 0 && k > 0 && k * k <= 255 && s > 0 &&
-                   dpool && idx && y && mean && invstd && scale && shift && dy && partial && coef,
+                   dpool && idx && y && mean && invstd && scale && shift && partial && coef,
                SSIP_ERR_ARG, "ssip_stem_pool_bn_bwd: bad arguments");
   const long M = (long)N * H * W;
   SSIP_REQUIRE(M * C / 8 < (1l << 31), SSIP_ERR_ARG, "ssip_stem_pool_bn_bwd: too large");
@@ -353,8 +353,9 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
                          pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, red_blocks, M, 1, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
-    hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
-                       (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);
+    if (dy)  // dy == nullptr: only dgamma/dbeta/coef (ssip_stem_bwd_wgrad forms dy on the fly)
+      hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
+                         (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);
   });
   return ::ssip::check_launch("stem_pool_bn_bwd");
 }

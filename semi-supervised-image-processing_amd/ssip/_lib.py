@@ -71,6 +71,8 @@ _SIGS = {
     "ssip_conv_dgrad_bn": (_c_int, [_PD, _c_int] + [_vp] * 10),
     "ssip_conv_wgrad_workspace_bytes": (_c_i64, [_PD]),
     "ssip_conv_wgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _vp]),
+    "ssip_stem_bwd_wgrad_supported": (_c_int, [_PD, _c_int]),
+    "ssip_stem_bwd_wgrad": (_c_int, [_PD, _c_int] + [_vp] * 8 + [_c_int] * 3 + [_vp, _c_i64, _vp]),
     "ssip_bn_finalize": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_eval_coeffs": (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_apply": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
@@ -132,7 +134,8 @@ def check(rc: int, what: str) -> None:
 
 
 # int-returning queries (not status codes)
-_NOT_STATUS = ("ssip_version", "ssip_conv_fwd_partial_tiles", "ssip_conv_dgrad_bn_partial_tiles")
+_NOT_STATUS = ("ssip_version", "ssip_conv_fwd_partial_tiles", "ssip_conv_dgrad_bn_partial_tiles",
+               "ssip_stem_bwd_wgrad_supported")
 
 
 def call(name: str, *args) -> int:

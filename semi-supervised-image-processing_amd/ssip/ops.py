@@ -199,6 +199,21 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
     call(*args)
 
 
+def stem_bwd_wgrad_supported(g: ConvGeom, dtype: torch.dtype) -> bool:
+    return bool(_lib.lib().ssip_stem_bwd_wgrad_supported(g.desc(), _DT[dtype]))
+
+
+def stem_bwd_wgrad(g: ConvGeom, dpool, idx, y, x, scale, shift, coef, dw, accumulate: bool, workspace) -> None:
+    """Stem wgrad with the BN-backward apply formed on the fly (include/ssip.h)."""
+    nbytes = workspace.numel() * workspace.element_size()
+    args = ("ssip_stem_bwd_wgrad", g.desc(), dtype_code(y), _p(dpool), _p(idx), _p(y), _p(x), _p(scale), _p(shift),
+            _p(coef), _p(dw), g.c_real, g.s_real, int(accumulate), _p(workspace), nbytes, stream_ptr())
+    if _timer is not None:
+        _timer.wrap("wgrad", g.flops(), call, *args)
+        return
+    call(*args)
+
+
 def weight_prep_batch(items, dtype: torch.dtype) -> None:
     """items: [(w_kcrs fp32, Cp, Sp, krsc or None, crsk or None)] -> one launch per 32."""
     for i in range(0, len(items), _lib.WPREP_MAX):

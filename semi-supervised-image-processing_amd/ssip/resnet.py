@@ -684,12 +684,31 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     # max-pool backward + ReLU mask + BN backward straight from the pooled gradient
     C1 = stem.geom.K
     dgam, dbet, acc = bn_grads(stem)
-    dy1 = torch.empty_like(stem.y)
     partial = torch.empty(ops.stem_pool_bn_bwd_partial_floats(N, P1, Q1, C1), device=dev, dtype=torch.float32)
+    w1 = stem.conv.weight
+    # the stem wgrad forms the BN-backward dy per tile in LDS (no full-resolution
+    # dy pass) where the geometry allows: ssip_stem_bwd_wgrad
+    fused = (w1.requires_grad and (mp.kernel_size, mp.stride, mp.padding) == (3, 2, 1)
+             and ops.stem_bwd_wgrad_supported(stem.geom, dt))
+    dy1 = None if fused else torch.empty_like(stem.y)
+    coef1 = coef_buf[: 3 * C1] if not fused else torch.empty(3 * C1, device=dev, dtype=torch.float32)
     ops.stem_pool_bn_bwd(N, P1, Q1, C1, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, stem.y,
                          stem.stats[0], stem.stats[1], stem.stats[2], stem.stats[3], stem.bn.weight.detach(), dgam,
-                         dbet, acc, dy1, partial, coef_buf[: 3 * C1], sv.pool_ymax)
-    conv_wgrad(stem, dy1)
+                         dbet, acc, dy1, partial, coef1, sv.pool_ymax)
+    if fused:
+        tgt, acc_w = _grad_target(w1, arena)
+        args = (stem.geom, dz, sv.pool_idx, stem.y, stem.x, stem.stats[2], stem.stats[3], coef1, tgt, acc_w,
+                workspace)
+        if side is None:
+            ops.stem_bwd_wgrad(*args)
+        else:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                ops.stem_bwd_wgrad(*args)
+            for t in (dz, coef1):
+                t.record_stream(side)
+    else:
+        conv_wgrad(stem, dy1)
     if hook is not None:
         hook([model.conv1.weight, model.bn1.weight, model.bn1.bias])
 

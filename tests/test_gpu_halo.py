@@ -157,3 +157,50 @@ def test_halo_wgrad(dev, shape, accumulate, monkeypatch):
     want = ref + (base.cpu().double() if accumulate else 0)
     assert _relerr(dw, want) < 1e-4
     assert _relerr(dw, dw0) < 1e-5
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_stem_bwd_wgrad_fused(dev, accumulate):
+    """ssip_stem_bwd_wgrad (dy formed per tile in LDS) against the unfused
+    ssip_stem_pool_bn_bwd apply pass + ssip_conv_wgrad on the same inputs
+    (224x224 geometry, batch 2).  dy is the same bf16 expression; only
+    fused-multiply-add contraction may differ -> dW rel-err <= 2e-3."""
+    torch.manual_seed(13)
+    N, C = 2, 64
+    dt = torch.bfloat16
+    g = ConvGeom(N, 230, 230, 4, C, 7, 8, 2, 0, 3, 7)
+    assert ops.stem_bwd_wgrad_supported(g, dt)
+    x = torch.randn(N, 230, 230, 4, device=dev).to(dt)
+    x[..., 3] = 0
+    y = torch.randn(N, 112, 112, C, device=dev).to(dt)
+    mean = torch.randn(C, device=dev) * 0.1
+    invstd = torch.rand(C, device=dev) + 0.5
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.1
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    pool = torch.empty(N, 56, 56, C, device=dev, dtype=dt)
+    idx = torch.empty(N, 56, 56, C, device=dev, dtype=torch.uint8)
+    ymax = torch.empty_like(pool)
+    ops.stem_bn_pool_fwd(N, 112, 112, C, 3, 2, 1, y, scale, shift, pool, idx, ymax)
+    dpool = torch.randn(N, 56, 56, C, device=dev).to(dt)
+    part = torch.empty(ops.stem_pool_bn_bwd_partial_floats(N, 112, 112, C), device=dev)
+    ws = torch.empty(ops.conv_wgrad_workspace_bytes(g), device=dev, dtype=torch.uint8)
+    base = torch.randn(C, 3, 7, 7, device=dev)
+
+    # unfused
+    dg, db, coef = torch.empty(C, device=dev), torch.empty(C, device=dev), torch.empty(3 * C, device=dev)
+    dy = torch.empty_like(y)
+    ops.stem_pool_bn_bwd(N, 112, 112, C, 3, 2, 1, dpool, idx, y, mean, invstd, scale, shift, gamma, dg, db, False, dy,
+                         part, coef, ymax)
+    dw0 = base.clone()
+    ops.conv_wgrad(g, dy, x, dw0, accumulate, ws)
+    # fused
+    dg2, db2, coef2 = torch.empty(C, device=dev), torch.empty(C, device=dev), torch.empty(3 * C, device=dev)
+    ops.stem_pool_bn_bwd(N, 112, 112, C, 3, 2, 1, dpool, idx, y, mean, invstd, scale, shift, gamma, dg2, db2, False,
+                         None, part, coef2, ymax)
+    dw = base.clone()
+    ops.stem_bwd_wgrad(g, dpool, idx, y, x, scale, shift, coef2, dw, accumulate, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(coef, coef2) and torch.equal(dg, dg2) and torch.equal(db, db2)
+    assert _relerr(dw.cpu(), dw0.cpu()) < 2e-3

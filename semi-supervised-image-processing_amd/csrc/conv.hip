@@ -1401,6 +1401,62 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // (channel, workgroup): [Ncols][G][3].  DGRAD epilogue: dx (+ add, which may
 // alias dx).
 // ---------------------------------------------------------------------------
+// BatchNorm statistics of a wave's output rows over the tiles of a
+// persistent workgroup: per lane (one column, the rows (l >> 4) * 4 + e of
+// each 16x16 fragment) a count and sums shifted by the lane's first value;
+// wave_merge turns them into {n, mean, M2} per column and combines the four
+// lane groups in fixed order (Chan).  Deterministic.
+template <int FM, int FN>
+struct WaveStats {
+  float n, k[FN], s1[FN], s2[FN];
+  __device__ __forceinline__ void reset() {
+    n = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) k[jj] = s1[jj] = s2[jj] = 0.f;
+  }
+  __device__ __forceinline__ void tile(const f32x4 (&acc)[FM][FN], uint32_t vmask) {
+    if (n == 0.f)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) k[jj] = acc[0][jj][0];
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = ((vmask >> (i * 4 + e)) & 1) ? acc[i][jj][e] - k[jj] : 0.f;
+          s1[jj] += d;
+          s2[jj] = __builtin_fmaf(d, d, s2[jj]);
+        }
+    n += (float)__builtin_popcount(vmask);
+  }
+  __device__ __forceinline__ void wave_merge(float& nw, float (&mean)[FN], float (&m2)[FN]) const {
+    nw = n;
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) {
+      mean[jj] = n > 0.f ? k[jj] + s1[jj] / n : 0.f;
+      m2[jj] = n > 0.f ? fmaxf(s2[jj] - s1[jj] * s1[jj] / n, 0.f) : 0.f;
+    }
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float nb = __shfl_xor(nw, off, 64);
+      const float nn = nw + nb;
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) {
+        const float mb = __shfl_xor(mean[jj], off, 64), qb = __shfl_xor(m2[jj], off, 64);
+        // combine in a fixed order (lower lane group first) so every lane gets the same bits
+        const bool lo = (threadIdx.x & off) == 0;
+        const float na_ = lo ? nw : nb, ma = lo ? mean[jj] : mb, qa = lo ? m2[jj] : qb;
+        const float nb_ = lo ? nb : nw, mb_ = lo ? mb : mean[jj], qb_ = lo ? qb : m2[jj];
+        const float d = mb_ - ma;
+        mean[jj] = nn > 0.f ? ma + d * (nb_ / nn) : 0.f;
+        m2[jj] = nn > 0.f ? qa + qb_ + d * d * (na_ * nb_ / nn) : 0.f;
+      }
+      nw = nn;
+    }
+  }
+};
+
 struct HaloArgs {
   const __bf16* X;    // [N][H][W][64]   (FWD: x, DGRAD: dy)
   const __bf16* Wt;   // [Ncols][9][64]  (FWD: w_krsc, DGRAD: w_crsk)
@@ -1498,9 +1554,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
       rec[2] = 0.f;
     }
   }
-  float st_n = 0.f, st_mean[FN], st_m2[FN];
-#pragma unroll
-  for (int jj = 0; jj < FN; ++jj) st_mean[jj] = st_m2[jj] = 0.f;
+  WaveStats<FM, FN> ws;
+  ws.reset();
   // this lane's output rows (rbase + 16 i + e): byte offset within a tile's
   // output block and validity (q < W of the padded grid), fixed for all tiles
   const int rbase = wm * WTM + kq * 4, cbase = wn * WTN + (lane & 15);
@@ -1593,51 +1648,23 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 
     // ---- epilogue
     if (a.partial && wrows > 0) {
-      // per-wave statistics of this tile (fp32 accumulators, valid rows),
-      // merged into the wave's running record in tile order (Chan)
-      const float nt = (float)wrows;
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s += ((vmask >> (i * 4 + e)) & 1) ? acc[i][jj][e] : 0.f;
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        const float mt = s / nt;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float d = acc[i][jj][e] - mt;
-            q += ((vmask >> (i * 4 + e)) & 1) ? d * d : 0.f;
-          }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        if (st_n == 0.f) {
-          st_mean[jj] = mt;
-          st_m2[jj] = q;
-        } else {
-          const float nn = st_n + nt, d = mt - st_mean[jj];
-          st_mean[jj] += d * (nt / nn);
-          st_m2[jj] += q + d * d * (st_n * nt / nn);
-        }
-      }
-      st_n += nt;
-      if (!prefetch) {  // the panel (or the workgroup's range) ends with this tile
+      // per-lane shifted sums over the fp32 accumulators of the valid rows;
+      // merged across the wave (and written) when the panel or range ends
+      ws.tile(acc, vmask);
+      if (!prefetch) {
+        float n, mean[FN], m2[FN];
+        ws.wave_merge(n, mean, m2);
         if (lane < 16) {
 #pragma unroll
           for (int jj = 0; jj < FN; ++jj) {
             const int c = jn * BN + cbase + jj * 16;
             float* rec = a.partial + ((long)c * G * WMW + (long)g * WMW + wm) * 3;
-            rec[0] = st_n;
-            rec[1] = st_mean[jj] * st_n;
-            rec[2] = st_m2[jj];
+            rec[0] = n;
+            rec[1] = mean[jj] * n;
+            rec[2] = m2[jj];
           }
         }
-        st_n = 0.f;
+        ws.reset();
       }
     }
     {
@@ -1795,9 +1822,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
       rec[2] = 0.f;
     }
   }
-  float st_n = 0.f, st_mean[FN], st_m2[FN];
-#pragma unroll
-  for (int jj = 0; jj < FN; ++jj) st_mean[jj] = st_m2[jj] = 0.f;
+  WaveStats<FM, FN> ws;
+  ws.reset();
 
   if (u0 < u1) {
     const int jn = u0 / a.tiles;
@@ -1843,49 +1869,23 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     if (a.partial && wrows > 0) {
-      const float nt = (float)wrows;
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) s += ((vmask >> (i * 4 + e)) & 1) ? acc[i][jj][e] : 0.f;
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        const float mt = s / nt;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float d = acc[i][jj][e] - mt;
-            q += ((vmask >> (i * 4 + e)) & 1) ? d * d : 0.f;
-          }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        if (st_n == 0.f) {
-          st_mean[jj] = mt;
-          st_m2[jj] = q;
-        } else {
-          const float nn = st_n + nt, d = mt - st_mean[jj];
-          st_mean[jj] += d * (nt / nn);
-          st_m2[jj] += q + d * d * (st_n * nt / nn);
-        }
-      }
-      st_n += nt;
+      // per-lane shifted sums over the fp32 accumulators of the valid rows;
+      // merged across the wave (and written) when the panel or range ends
+      ws.tile(acc, vmask);
       if (!prefetch) {
+        float n, mean[FN], m2[FN];
+        ws.wave_merge(n, mean, m2);
         if (lane < 16) {
 #pragma unroll
           for (int jj = 0; jj < FN; ++jj) {
             const int c = jn * BN + cbase + jj * 16;
             float* rec = a.partial + ((long)c * G * WMW + (long)g * WMW + wm) * 3;
-            rec[0] = st_n;
-            rec[1] = st_mean[jj] * st_n;
-            rec[2] = st_m2[jj];
+            rec[0] = n;
+            rec[1] = mean[jj] * n;
+            rec[2] = m2[jj];
           }
         }
-        st_n = 0.f;
+        ws.reset();
       }
     }
     {

@@ -9,6 +9,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import os
 import torch
 
 from . import _lib
@@ -35,7 +36,9 @@ def _p(t: Optional[torch.Tensor]):
 
 
 def stream_ptr() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """Raw hipStream_t of the calling thread's current stream (the plain
+    torch.cuda.current_stream() path costs ~8 us per call; a step makes ~130)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 # ---------------------------------------------------------------------------
@@ -77,6 +80,9 @@ def set_conv_timer(t):
 # ---------------------------------------------------------------------------
 # convolution
 # ---------------------------------------------------------------------------
+_desc_cache = {}  # ConvGeom -> its C descriptor (passed by reference, never written by the library)
+
+
 @dataclass(frozen=True)
 class ConvGeom:
     N: int
@@ -102,21 +108,41 @@ class ConvGeom:
     def desc(self) -> ConvDesc:
         # the padded stem column (s = 7) must not change the output width:
         # Q is computed with the real filter width; the kernel only needs P/Q.
-        d = ConvDesc(self.N, self.H, self.W, self.C, self.K, self.R, self.S, self.stride, self.pad, self.P, self.Q)
+        d = _desc_cache.get(self)
+        if d is None:
+            d = _desc_cache[self] = ConvDesc(self.N, self.H, self.W, self.C, self.K, self.R, self.S, self.stride,
+                                             self.pad, self.P, self.Q)
         return d
 
     def flops(self) -> int:
         return 2 * self.N * self.P * self.Q * self.K * self.c_real * self.R * self.s_real
 
 
+# plans depend only on the geometry (and on SSIP_* tuning variables, read at
+# each call by the library): memoised per (geometry, environment) for the host path
+_plan_cache = {}
+
+
+def _plan_env():
+    return (os.environ.get("SSIP_HALO"), os.environ.get("SSIP_CONV_FORCE"))
+
+
 def conv_fwd_partial_floats(g: ConvGeom) -> int:
-    return int(_lib.lib().ssip_conv_fwd_partial_floats(g.desc()))
+    key = ("pf", g, _plan_env())
+    v = _plan_cache.get(key)
+    if v is None:
+        v = _plan_cache[key] = int(_lib.lib().ssip_conv_fwd_partial_floats(g.desc()))
+    return v
 
 
 def conv_fwd_partial_tiles(g: ConvGeom, dtype: torch.dtype) -> int:
-    t = int(_lib.lib().ssip_conv_fwd_partial_tiles(g.desc(), _DT[dtype]))
-    if t <= 0:
-        raise RuntimeError(_lib.lib().ssip_last_error().decode())
+    key = ("pt", g, dtype, _plan_env())
+    t = _plan_cache.get(key)
+    if t is None:
+        t = int(_lib.lib().ssip_conv_fwd_partial_tiles(g.desc(), _DT[dtype]))
+        if t <= 0:
+            raise RuntimeError(_lib.lib().ssip_last_error().decode())
+        _plan_cache[key] = t
     return t
 
 

@@ -479,6 +479,19 @@ def _wgrad_stream(dev: torch.device):
     return st
 
 
+def _stage_params(model: SSIPResNet):
+    """(trunk parameters, per-stage parameter lists: stem, then each block),
+    cached on the model (the module tree is fixed; requires_grad is read
+    from the parameters at every call)."""
+    st = getattr(model, "_stage_params_cache", None)
+    if st is None:
+        stages = [[model.conv1, model.bn1]] + [[m for m in b.modules() if m is not b] for b in model.blocks()]
+        per = [[p for m in mods for p in m.parameters(recurse=False)] for mods in stages]
+        st = ([p for ps in per for p in ps], per)
+        object.__setattr__(model, "_stage_params_cache", st)
+    return st
+
+
 def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     side = _wgrad_stream(dlogits.device)
     if side is None:
@@ -500,8 +513,8 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     C = sv.last.shape[-1]
     J = fc.out_features
     # which stages need input gradients: anything downstream of the first trainable layer
-    trunk = [model.conv1, model.bn1] + [m for b in model.blocks() for m in b.modules() if m is not b]
-    trunk_trainable = any(p.requires_grad for m in trunk for p in m.parameters(recurse=False))
+    trunk_params, stage_params = _stage_params(model)
+    trunk_trainable = any(p.requires_grad for p in trunk_params)
     fc_w = fc.weight
     dw = db = None
     accw = accb = False
@@ -533,10 +546,9 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         hook(list(fc.parameters()))
 
     # earliest trainable stage decides where dgrad can stop
-    stage_params = [[model.conv1, model.bn1]] + [[m for m in b.modules() if m is not b] for b in model.blocks()]
     first_trainable = None
-    for i, mods in enumerate(stage_params):
-        if any(p.requires_grad for m in mods for p in m.parameters(recurse=False)):
+    for i, ps in enumerate(stage_params):
+        if any(p.requires_grad for p in ps):
             first_trainable = i
             break
 

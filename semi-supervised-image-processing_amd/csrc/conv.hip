@@ -1469,7 +1469,7 @@ struct HaloArgs {
 };
 
 constexpr int HALO_XBUF = 44 * 1024;
-constexpr int HALO_WMW = 4;
+constexpr int HALO_WMW = 8;  // BN records per (channel, workgroup) of the halo / stem forwards (>= wave rows)
 
 // X-row LDS image: pixel px's 128-B row, 16-B slot s at s ^ 2((px >> 1) & 3).
 // Fragment reads start at any pixel (tap shifts); with this swizzle the 16
@@ -1489,7 +1489,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   constexpr int BM = 256, BN = 64;
   constexpr int WTM = BM / WMW, WTN = BN / WNW, FM = WTM / 16, FN = WTN / 16;
   constexpr int B_BYTES = 9 * BN * 128;
-  static_assert(FM >= 1 && FN >= 1 && (NW == 4 || NW == 8), "bad halo wave tile");
+  static_assert(FM >= 1 && FN >= 1 && (NW == 4 || NW == 8 || NW == 16) && WMW <= HALO_WMW, "bad halo wave tile");
   static_assert(B_BYTES + 2 * HALO_XBUF <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[B_BYTES + 2 * HALO_XBUF];
   char* const Bs = smem;
@@ -1547,8 +1547,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   // zero this workgroup's, then lanes < 16 of each wave keep the running
   // {n, mean, M2} of their FN columns over the wave's rows of every tile
   if (a.partial) {
-    for (int c = tid; c < a.Ncols * WMW; c += NT) {
-      float* rec = a.partial + ((long)(c / WMW) * G * WMW + (long)g * WMW + c % WMW) * 3;
+    for (int c = tid; c < a.Ncols * HALO_WMW; c += NT) {
+      float* rec = a.partial + ((long)(c / HALO_WMW) * G * HALO_WMW + (long)g * HALO_WMW + c % HALO_WMW) * 3;
       rec[0] = 0.f;
       rec[1] = 0.f;
       rec[2] = 0.f;
@@ -1658,7 +1658,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
           for (int jj = 0; jj < FN; ++jj) {
             const int c = jn * BN + cbase + jj * 16;
-            float* rec = a.partial + ((long)c * G * WMW + (long)g * WMW + wm) * 3;
+            float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
             rec[0] = n;
             rec[1] = mean[jj] * n;
             rec[2] = m2[jj];
@@ -1815,8 +1815,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
   for (int r = wm * WTM; r < wm * WTM + WTM; ++r) wrows += (r % STEM_QP < a.Q) ? 1 : 0;
 
   if (a.partial) {
-    for (int c = tid; c < a.Ncols * WMW; c += NT) {
-      float* rec = a.partial + ((long)(c / WMW) * G * WMW + (long)g * WMW + c % WMW) * 3;
+    for (int c = tid; c < a.Ncols * HALO_WMW; c += NT) {
+      float* rec = a.partial + ((long)(c / HALO_WMW) * G * HALO_WMW + (long)g * HALO_WMW + c % HALO_WMW) * 3;
       rec[0] = 0.f;
       rec[1] = 0.f;
       rec[2] = 0.f;
@@ -1879,7 +1879,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
 #pragma unroll
           for (int jj = 0; jj < FN; ++jj) {
             const int c = jn * BN + cbase + jj * 16;
-            float* rec = a.partial + ((long)c * G * WMW + (long)g * WMW + wm) * 3;
+            float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
             rec[0] = n;
             rec[1] = mean[jj] * n;
             rec[2] = m2[jj];
@@ -2811,11 +2811,17 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   h.TR = hp.TR; h.tiles = hp.tiles; h.units = hp.units;
   h.flip = mode == MODE_DGRAD ? 1 : 0;
   { const char* dbg = getenv("SSIP_HALO_DBG"); h.dbg = dbg ? atoi(dbg) : 0; }
+  // 8 waves of 64x32 by default.  SSIP_HALO_WAVES=16 (16 waves of 32x32, 4 per
+  // SIMD, VGPR-capped: spills) is ~10 % faster in isolation but 3 % slower in
+  // the step, where the side streams' kernels run beside it; 4 = 64x64 waves
   const char* e = getenv("SSIP_HALO_WAVES");
-  if (e && atoi(e) == 4)
+  const int nw = e ? atoi(e) : 8;
+  if (nw == 4)
     hipLaunchKernelGGL((conv_halo_kernel<4, 1>), dim3(hp.G), dim3(256), 0, st, h);
-  else
+  else if (nw == 8)
     hipLaunchKernelGGL((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<8, 2>), dim3(hp.G), dim3(1024), 0, st, h);
   return ::ssip::check_launch("conv_halo");
 }
 

@@ -14,8 +14,10 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 
 
 def family(n):
-    if "conv_halo_wgrad_kernel" in n:
+    if "conv_halo_wgrad_kernel" in n or "conv_stem_wgrad_kernel" in n:
         return "conv_wgrad"
+    if "conv_stem_bwd_wgrad_kernel" in n:
+        return "conv_wgrad (stem, fused BN-backward apply)"
     if "conv_stem_halo_kernel" in n:
         return "conv_fwd"
     if "conv_halo_kernel" in n:

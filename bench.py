@@ -179,7 +179,8 @@ def main():
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_note": "bytes per step for the same conv family, PMC FETCH_SIZE*2 + WRITE_SIZE "
                                          "(profiles/r1_pmc_traffic.json; Infinity-Cache hits are counted)",
-                         "kernel": "conv family: conv_glds / conv_halo / conv_stem_halo / conv_halo_wgrad (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
+                         "kernel": "conv family: conv_glds / conv_halo / conv_stem_halo / conv_halo_wgrad / "
+                                   "conv_stem_bwd_wgrad (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
                                    f"in {conv_ms:.3f} ms"},
             "cpu_baseline": cpu,

@@ -12,7 +12,7 @@ import collections, csv, json, sys
 
 def family(n):
     for k in ("conv_gemm_kernel", "conv_glds_kernel", "conv_halo_kernel", "conv_stem_halo_kernel",
-              "conv_halo_wgrad_kernel"):
+              "conv_halo_wgrad_kernel", "conv_stem_wgrad_kernel", "conv_stem_bwd_wgrad_kernel"):
         if k in n:
             return "conv"
     if "wgrad_reduce" in n:

@@ -20,7 +20,9 @@ CPU restatement of the same step (oracle/step_oracle.py) on rank 0.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
+import re
 import os
 import sys
 import time
@@ -36,6 +38,11 @@ import torch.distributed as dist  # noqa: E402
 GFLOP_PER_IMG_TRAIN = 10.64535   # R18 224² fwd+dgrad+wgrad (no stem dgrad)
 GFLOP_PER_IMG_FWD = 3.627125
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def _round_of(path: str) -> int:
+    m = re.search(r"r(\d+)_pmc_traffic", os.path.basename(path))
+    return int(m.group(1)) if m else -1
 
 
 def parse():
@@ -133,22 +140,30 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
 
     # HBM traffic of the same family from the committed rocprofv3 PMC passes of
-    # this workload (tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE, separate
-    # passes, per step) — counters cannot be read from inside the run itself
-    traffic = None
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_pmc_traffic.json")
-    if os.path.exists(pmc):
+    # THIS workload (tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE, separate
+    # passes, per step): counters cannot be read from inside the run itself, so
+    # a file is used only when its `_workload` key equals this run's; else null
+    workload_key = f"semi_consistency_{args.arch}_{S} bs{args.batch} labeled{Bl} {args.dtype}"
+    traffic, traffic_src = None, None
+    for pmc in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                             "r*_pmc_traffic.json")), key=_round_of):
         with open(pmc) as f:
-            traffic = json.load(f).get("conv", {}).get("total_bytes")
+            d = json.load(f)
+        if d.get("_workload") == workload_key:
+            traffic, traffic_src = d.get("conv", {}).get("total_bytes"), os.path.basename(pmc)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.step_oracle import time_cpu_step
 
-        threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
-        c = time_cpu_step(Bl=16, Bu=16, steps=4, threads=threads)
+        # the host cores this process may run on (the box's CPU share), capped by
+        # OMP_NUM_THREADS when set; the machine's total is reported beside it
+        avail = len(os.sched_getaffinity(0))
+        threads = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)))
+        c = time_cpu_step(Bl=Bl, Bu=Bu, steps=5, warmup=2, threads=threads)
         cpu = {"value": round(c["value"], 3), "unit": "images/s", "cores": c["threads"], "kind": "port",
-               "sample": c["sample"]}
+               "sample": c["sample"], "host_cpus_affinity": avail, "host_cpus_total": os.cpu_count(),
+               "step_times_s": [round(t, 3) for t in c["step_times_s"]]}
 
     if rank == 0:
         imgs = args.batch * world * args.steps
@@ -177,8 +192,9 @@ def main():
                        if (args.arch, S) == ("resnet18", 224) else round(conv_flops / 1e9, 1)},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "traffic_note": "bytes per step for the same conv family, PMC FETCH_SIZE*2 + WRITE_SIZE "
-                                         "(profiles/r1_pmc_traffic.json; Infinity-Cache hits are counted)",
+                         "traffic_note": ("bytes per step for the same conv family, PMC FETCH_SIZE*2 + WRITE_SIZE "
+                                          f"(profiles/{traffic_src}; Infinity-Cache hits are counted)")
+                         if traffic_src else f"no committed PMC passes for workload '{workload_key}'",
                          "kernel": "conv family: conv_glds / conv_halo / conv_stem_halo / conv_halo_wgrad / "
                                    "conv_stem_bwd_wgrad (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "

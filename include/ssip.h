@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 3
+#define SSIP_ABI_VERSION 4
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -95,6 +95,12 @@ int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d);
 /* dw_kcrs (fp32, torchvision layout [K][c_real][R][s_real]) (+)= dW */
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
                     int s_real, int accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Name of the kernel a pass selects for this geometry (mode 0 = fwd,
+ * 1 = dgrad, 2 = wgrad), e.g. "glds<fwd,256x256,4x2,2,splits=1>" or
+ * "halo<dgrad,TR=4,G=256>": lets tests assert that a shape exercises the
+ * production kernel the benchmark runs. */
+int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* buf, int buflen);
 
 /* ------------------------------------------------------------------------
  * BatchNorm2d (train / eval) fused with ReLU and the residual add.

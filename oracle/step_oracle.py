@@ -70,9 +70,13 @@ def view_from_draw(img: Image.Image, size: int, flip: bool, angle, brightness: f
 
 
 def semi_step_reference(model, opt, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.ndarray, draws_l, draws_w, draws_s,
-                        size: int, tau: float, lambda_u: float) -> torch.Tensor:
+                        size: int, tau: float, lambda_u: float, pseudo_override=None, out: dict = None) -> torch.Tensor:
     """One joint step with explicit view parameters (draws: (flip, angle,
-    brightness, contrast, cutout) tuples).  Returns [total, L_l, L_u, mask count]."""
+    brightness, contrast, cutout) tuples).  Returns [total, L_l, L_u, mask count].
+
+    pseudo_override: use these pseudo-labels instead of the weak view's argmax
+    (a parity test pins near-tied samples to the device's picks); out (dict):
+    receives the weak logits 'zw', the joint logits 'z' and the pseudo-labels."""
     xl = torch.stack([view_from_draw(Image.fromarray(a), size, *d) for a, d in zip(x_l, draws_l)])
     xw = torch.stack([view_from_draw(Image.fromarray(a), size, *d) for a, d in zip(x_u, draws_w)])
     xs = torch.stack([view_from_draw(Image.fromarray(a), size, *d) for a, d in zip(x_u, draws_s)])
@@ -88,9 +92,13 @@ def semi_step_reference(model, opt, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.
             b.running_var.copy_(rv)
             b.num_batches_tracked.copy_(nb)
     conf, pseudo = torch.softmax(zw, 1).max(1)
+    if pseudo_override is not None:
+        pseudo = pseudo_override.to(pseudo.device, pseudo.dtype)
     mask = (conf >= tau).to(dt)
     opt.zero_grad(set_to_none=True)
     z = model(torch.cat([xl, xs], 0))
+    if out is not None:
+        out.update(zw=zw.detach(), z=z.detach(), pseudo=pseudo)
     Bl = xl.shape[0]
     l_l = F.cross_entropy(z[:Bl], y_l)
     l_u = (F.cross_entropy(z[Bl:], pseudo, reduction="none") * mask).mean()
@@ -139,19 +147,28 @@ class CpuSemiStep:
         return float(loss)
 
 
-def time_cpu_step(Bl: int = 8, Bu: int = 8, steps: int = 3, threads: int = 16, seed: int = 0) -> Dict:
-    """Images/sec of the CPU step on a bounded sample (steps x (Bl+Bu) images)."""
+def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2, threads: int = 16,
+                  seed: int = 0) -> Dict:
+    """Images/sec of the CPU step (the full per-GPU batch,
+    warm-up steps, then the MEDIAN of the timed steps) on a bounded sample of
+    steps x (Bl + Bu) images."""
+    import statistics
+
     torch.set_num_threads(threads)
     rng = np.random.default_rng(seed)
     x_l = rng.integers(0, 256, (Bl, 224, 224, 3), dtype=np.uint8)
     x_u = rng.integers(0, 256, (Bu, 224, 224, 3), dtype=np.uint8)
     y_l = torch.from_numpy(rng.integers(0, 2, Bl))
     step = CpuSemiStep()
-    step(x_l, y_l, x_u)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(warmup):
         step(x_l, y_l, x_u)
-    dt = (time.perf_counter() - t0) / steps
-    return {"value": (Bl + Bu) / dt, "step_s": dt, "threads": torch.get_num_threads(),
-            "sample": f"{steps} steps x ({Bl} labelled + {Bu} unlabelled) 224x224 uint8 images, "
-                      f"PIL views + torch fp32 ResNet-18 fwd/bwd + AdamW"}
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        step(x_l, y_l, x_u)
+        times.append(time.perf_counter() - t0)
+    dt = statistics.median(times)
+    return {"value": (Bl + Bu) / dt, "step_s": dt, "threads": torch.get_num_threads(), "step_times_s": times,
+            "sample": f"median of {steps} timed steps after {warmup} warm-up, each {Bl} labelled + {Bu} "
+                      f"unlabelled 224x224 uint8 images: PIL weak/strong views + torch fp32 ResNet-18 weak forward "
+                      f"+ joint fwd/bwd + AdamW (oracle/step_oracle.py)"}

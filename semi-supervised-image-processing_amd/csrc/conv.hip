@@ -2815,7 +2815,15 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   // SIMD, VGPR-capped: spills) is ~10 % faster in isolation but 3 % slower in
   // the step, where the side streams' kernels run beside it; 4 = 64x64 waves
   const char* e = getenv("SSIP_HALO_WAVES");
-  const int nw = e ? atoi(e) : 8;
+  int nw = 8;
+  if (e && e[0]) {
+    char* end = nullptr;
+    nw = (int)strtol(e, &end, 10);
+    if (*end || (nw != 4 && nw != 8 && nw != 16)) {
+      ::ssip::set_error("SSIP_HALO_WAVES=\"%s\": must be 4, 8 or 16", e);
+      return SSIP_ERR_ARG;
+    }
+  }
   if (nw == 4)
     hipLaunchKernelGGL((conv_halo_kernel<4, 1>), dim3(hp.G), dim3(256), 0, st, h);
   else if (nw == 8)
@@ -3062,6 +3070,49 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace, hp.G,
                      64, 224, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
   return ::ssip::check_launch("wgrad_reduce");
+}
+
+
+/* Which kernel a conv pass selects for this geometry (tests / tuning): writes a
+ * NUL-terminated name such as "glds<fwd,256x256,4x2,2>" or "halo<fwd>" into buf. */
+int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* buf, int buflen) {
+  SSIP_REQUIRE(buf && buflen > 0, SSIP_ERR_ARG, "ssip_conv_kernel_name: no buffer");
+  SSIP_REQUIRE(mode >= 0 && mode <= 2, SSIP_ERR_ARG, "ssip_conv_kernel_name: mode must be 0 (fwd), 1 (dgrad), 2 (wgrad)");
+  static const char* mname[3] = {"fwd", "dgrad", "wgrad"};
+  const int m = mode == 0 ? MODE_FWD : mode == 1 ? MODE_DGRAD : MODE_WGRAD;
+  HaloPlan hp;
+  if (m == MODE_FWD && halo_plan(MODE_FWD, d, dtype, hp)) {
+    snprintf(buf, buflen, "halo<fwd,TR=%d,G=%d>", hp.TR, hp.G);
+    return SSIP_OK;
+  }
+  if (m == MODE_FWD && stem_plan(d, dtype, hp)) {
+    snprintf(buf, buflen, "stem_halo<fwd,G=%d>", hp.G);
+    return SSIP_OK;
+  }
+  if (m == MODE_DGRAD && halo_plan(MODE_DGRAD, d, dtype, hp)) {
+    snprintf(buf, buflen, "halo<dgrad,TR=%d,G=%d>", hp.TR, hp.G);
+    return SSIP_OK;
+  }
+  if (m == MODE_WGRAD && stem_wg_plan(d, dtype, hp)) {
+    snprintf(buf, buflen, "stem_wgrad<G=%d>", hp.G);
+    return SSIP_OK;
+  }
+  if (m == MODE_WGRAD && halo_wg_plan(d, dtype, hp)) {
+    snprintf(buf, buflen, "halo_wgrad<TR=%d,G=%d>", hp.TR, hp.G);
+    return SSIP_OK;
+  }
+  Plan pl;
+  int rc = plan_conv(m, d, elem_bytes_of(dtype), pl);
+  if (rc) return rc;
+  if (m == MODE_FWD && pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
+  if (m == MODE_DGRAD) {
+    phase_split(pl, d);
+    if (pl.stages > 0 && ((d->stride != 1 && !pl.args.phased) || d->R * d->S > 32)) fallback_regstaged(pl);
+  }
+  snprintf(buf, buflen, "%s<%s,%dx%d,%dx%d,%d%s%s,splits=%d>", pl.stages > 0 ? "glds" : "regstaged", mname[mode],
+           pl.bm, pl.bn, pl.wmw, pl.wnw, pl.stages, pl.conv1 ? ",stem" : "", pl.args.phased ? ",phased" : "",
+           pl.splits);
+  return SSIP_OK;
 }
 
 }  // extern "C"

@@ -50,6 +50,9 @@ def base_parser(doc: str, weak_required: bool) -> argparse.ArgumentParser:
                    help="Activation dtype of the HIP kernels (fp32 = reference numerics, bf16 = throughput).")
     p.add_argument("--weights", type=Path, default=None,
                    help="Local torchvision resnet18 state_dict standing in for the IMAGENET1K_V1 download.")
+    p.add_argument("--random-init", action="store_true",
+                   help="Allow the seeded random backbone when no ImageNet weights are available locally "
+                        "(otherwise a missing download is an error, as in the reference).")
     return p
 
 
@@ -75,5 +78,5 @@ def to_config(a, semi: bool) -> TrainingConfig:
         baseline_checkpoint=o / "models/baseline_resnet18.pt",
         semi_checkpoint=o / "models/semi_resnet18.pt",
         unlabeled_cohort_csv=a.unlabeled_cohort_csv if semi else None,
-        dtype=a.dtype, weights=a.weights,
+        dtype=a.dtype, weights=a.weights, random_init=a.random_init,
     )

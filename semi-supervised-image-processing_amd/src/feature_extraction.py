@@ -78,6 +78,7 @@ class ExtractionResults:
     records: List[ImageRecord]
     failures: List[Path]
     per_file_times: List[float]
+    weights: str = BACKBONE_WEIGHTS   # what the backbone was initialised from (metadata.json "weights")
 
 
 def configure_logging(verbose: bool = False) -> None:
@@ -120,9 +121,15 @@ def build_transform(dtype: torch.dtype = torch.float32) -> GpuTransform:
                         std=IMAGENET_STD)
 
 
-def load_model(device: torch.device, dtype: str = "fp32", weights: Optional[Path] = None) -> SSIPResNet:
+def load_model(device: torch.device, dtype: str = "fp32", weights: Optional[Path] = None,
+               allow_random_init: bool = False) -> SSIPResNet:
     """Frozen eval-mode ResNet-18 returning the [B,512,1,1] avgpool output
-    (the reference's nn.Sequential(children()[:-1]))."""
+    (the reference's nn.Sequential(children()[:-1]), feature_extraction.py:210-227).
+    The IMAGENET1K_V1 download of the reference is a local state_dict here
+    (`weights` / $SSIP_RESNET18_WEIGHTS); without one this raises, as the
+    reference's failed download does, unless the seeded random backbone was
+    opted in to (--random-init / $SSIP_ALLOW_RANDOM_INIT=1); metadata.json's
+    "weights" then says so."""
     import os
 
     path = weights or os.environ.get(WEIGHTS_ENV)
@@ -130,9 +137,15 @@ def load_model(device: torch.device, dtype: str = "fp32", weights: Optional[Path
     model = SSIPResNet("resnet18", num_classes=1000, dtype=dtype)
     if path and Path(path).exists():
         model.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
-    else:
+        model.init_source = BACKBONE_WEIGHTS
+    elif allow_random_init or os.environ.get("SSIP_ALLOW_RANDOM_INIT") == "1":
         logging.warning("%s unavailable offline; embeddings use the seeded (seed %d) random initialisation "
-                        "(set %s to a local state_dict)", BACKBONE_WEIGHTS, RNG_SEED, WEIGHTS_ENV)
+                        "(opted in)", BACKBONE_WEIGHTS, RNG_SEED)
+        model.init_source = f"random_init(seed={RNG_SEED})"
+    else:
+        raise RuntimeError(f"{BACKBONE_WEIGHTS} is a network download and no local copy was given: pass --weights "
+                           f"<torchvision resnet18 state_dict> or set {WEIGHTS_ENV}, or opt in to the seeded random "
+                           "backbone with --random-init (or SSIP_ALLOW_RANDOM_INIT=1)")
     model.eval()
     for p in model.parameters():
         p.requires_grad_(False)
@@ -156,8 +169,8 @@ def batched(items: Sequence, batch_size: int) -> Iterable[Sequence]:
 
 def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_size: int = BATCH_SIZE,
                        dtype: str = "fp32", weights: Optional[Path] = None,
-                       decode_threads: int = 8) -> ExtractionResults:
-    model = load_model(device, dtype, weights)
+                       decode_threads: int = 8, allow_random_init: bool = False) -> ExtractionResults:
+    model = load_model(device, dtype, weights, allow_random_init)
     tf = build_transform(model.compute_dtype)
     embeddings: List[np.ndarray] = []
     kept: List[ImageRecord] = []
@@ -198,7 +211,7 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
         raise RuntimeError("No embeddings were generated; all images failed to decode?")
     mat = np.concatenate(embeddings, 0)
     logging.info("Computed embeddings with shape %s", mat.shape)
-    return ExtractionResults(mat, kept, failures, times)
+    return ExtractionResults(mat, kept, failures, times, model.init_source)
 
 
 def compute_dataset_digest(records: Sequence[ImageRecord]) -> str:
@@ -255,7 +268,7 @@ def save_artifacts(results: ExtractionResults, stats: Dict[str, float], probe: L
     np.save(EMBEDDING_ARRAY_PATH, results.embeddings.astype(np.float32))
     pd.DataFrame([{"index": i, "path": str(r.relative_path), "bucket": r.bucket, "label": r.label}
                   for i, r in enumerate(results.records)]).to_csv(EMBEDDING_CSV_PATH, index=False)
-    meta = {"backbone": BACKBONE_NAME, "weights": BACKBONE_WEIGHTS, "layer": BACKBONE_LAYER,
+    meta = {"backbone": BACKBONE_NAME, "weights": results.weights, "layer": BACKBONE_LAYER,
             "embedding_dimension": int(results.embeddings.shape[1]), "input_resize": TARGET_RESIZE,
             "input_crop": TARGET_CROP, "normalization_mean": IMAGENET_MEAN, "normalization_std": IMAGENET_STD,
             "channel_policy": "No conversion (assumes RGB inputs)",
@@ -273,7 +286,7 @@ def save_artifacts(results: ExtractionResults, stats: Dict[str, float], probe: L
     nb = "\n".join(lines) if probe else "No neighbors computed (insufficient samples)."
     SUMMARY_NOTE_PATH.write_text(f"""# Feature Extraction Summary
 
-- Backbone: {BACKBONE_NAME} ({BACKBONE_WEIGHTS})
+- Backbone: {BACKBONE_NAME} ({results.weights})
 - Layer: global average pooled features ({results.embeddings.shape[1]}-D)
 - Input spec: resize {TARGET_RESIZE} → center crop {TARGET_CROP}, ImageNet normalization
 - Batch size: {BATCH_SIZE}
@@ -308,6 +321,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     p.add_argument("--verbose", action="store_true", help="Enable verbose logging")
     p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--weights", type=Path, default=None)
+    p.add_argument("--random-init", action="store_true",
+                   help="Allow the seeded random backbone when no ImageNet weights are available locally")
     return p.parse_args(argv)
 
 
@@ -321,7 +336,7 @@ def main(argv=None) -> None:
     records = discover_image_records(args.data_dir)
     t0 = time.perf_counter()
     res = extract_embeddings(records, device=device, batch_size=args.batch_size, dtype=args.dtype,
-                             weights=args.weights)
+                             weights=args.weights, allow_random_init=args.random_init)
     logging.info("Completed embedding extraction in %.2f seconds", time.perf_counter() - t0)
     stats = run_sanity_checks(res.embeddings)
     probe = nearest_neighbor_probe(res.embeddings, res.records)

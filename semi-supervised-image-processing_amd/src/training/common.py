@@ -99,6 +99,7 @@ class TrainingConfig:
     # ssip extensions (optional, defaults keep reference numerics)
     dtype: str = "fp32"
     weights: Optional[Path] = None
+    random_init: bool = False   # opt in to the seeded random backbone when no ImageNet weights are local
 
 
 # ---------------------------------------------------------------------------
@@ -242,22 +243,39 @@ def prepare_dataloaders(strong_data_dir: Path, transforms_map, batch_size: int, 
 # ---------------------------------------------------------------------------
 
 _WEIGHTS_ENV = "SSIP_RESNET18_WEIGHTS"
+_RANDOM_INIT_ENV = "SSIP_ALLOW_RANDOM_INIT"
+
+
+def random_init_allowed(flag: bool = False) -> bool:
+    return bool(flag) or os.environ.get(_RANDOM_INIT_ENV) == "1"
 
 
 def create_model(num_classes: int, pretrained: bool = True, dtype: str = "fp32",
-                 weights: Optional[Path] = None) -> SSIPResNet:
+                 weights: Optional[Path] = None, allow_random_init: bool = False) -> SSIPResNet:
     """torchvision resnet18 (+ new fc) semantics and RNG consumption.  The
-    ImageNet weights are a network download in the reference; here they
-    load from `weights` or $SSIP_RESNET18_WEIGHTS (a torchvision state_dict),
-    otherwise the seeded random initialisation is kept (with a warning)."""
+    ImageNet weights are a network download in the reference
+    (ResNet18_Weights.IMAGENET1K_V1, common.py:299-304), which fails offline;
+    here they load from `weights` or $SSIP_RESNET18_WEIGHTS (a torchvision
+    state_dict).  Without either, pretrained=True raises like the
+    reference's failed download, unless the caller opted in to the seeded
+    random initialisation (allow_random_init / --random-init /
+    $SSIP_ALLOW_RANDOM_INIT=1); the model then records it in `init_source`."""
     model = SSIPResNet("resnet18", num_classes=1000, dtype=dtype)
+    model.init_source = "random_init"
     if pretrained:
         path = weights or os.environ.get(_WEIGHTS_ENV)
         if path and Path(path).exists():
             model.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+            model.init_source = f"state_dict:{path}"
+        elif random_init_allowed(allow_random_init):
+            warnings.warn("ResNet18_Weights.IMAGENET1K_V1 unavailable offline; using the seeded random init "
+                          "(opted in)")
+            LOGGER.warning("Backbone: seeded random initialisation (no ImageNet weights; opted in)")
         else:
-            warnings.warn("ResNet18_Weights.IMAGENET1K_V1 unavailable offline; using seeded random init "
-                          f"(set {_WEIGHTS_ENV} or --weights to a local state_dict)")
+            raise RuntimeError(
+                "ResNet18_Weights.IMAGENET1K_V1 is a network download and no local copy was given: pass --weights "
+                f"<torchvision resnet18 state_dict> or set {_WEIGHTS_ENV}, or opt in to the seeded random "
+                f"initialisation with --random-init (or {_RANDOM_INIT_ENV}=1)")
     replace_fc(model, num_classes)
     return model
 

@@ -138,7 +138,8 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
     criterion = CrossEntropyLoss()
 
     # baseline
-    baseline = create_model(num_classes, pretrained=True, dtype=config.dtype, weights=config.weights).to(device)
+    baseline = create_model(num_classes, pretrained=True, dtype=config.dtype, weights=config.weights,
+                           allow_random_init=config.random_init).to(device)
     opt = make_optimizer(baseline, config.learning_rate, config.weight_decay)
     sch = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", patience=2, factor=0.5)
     t0 = time.time()
@@ -168,7 +169,8 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
                                collate_fn=Collate(tfm["train"]))
 
     # frozen-backbone pretrain (BN still in train mode), then fine-tune
-    semi = create_model(num_classes, pretrained=True, dtype=config.dtype, weights=config.weights).to(device)
+    semi = create_model(num_classes, pretrained=True, dtype=config.dtype, weights=config.weights,
+                           allow_random_init=config.random_init).to(device)
     for name, p in semi.named_parameters():
         if not name.startswith("fc"):
             p.requires_grad = False

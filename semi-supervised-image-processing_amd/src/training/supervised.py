@@ -41,7 +41,8 @@ def run_supervised(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
     if config.positive_class not in base.class_to_idx:
         raise ValueError(f"Positive class '{config.positive_class}' not found in dataset classes: {base.classes}")
     pos_index = int(base.class_to_idx[config.positive_class])
-    model = create_model(len(base.classes), pretrained=True, dtype=config.dtype, weights=config.weights).to(device)
+    model = create_model(len(base.classes), pretrained=True, dtype=config.dtype, weights=config.weights,
+                           allow_random_init=config.random_init).to(device)
     criterion = CrossEntropyLoss()
     opt = make_optimizer(model, config.learning_rate, config.weight_decay)
     sch = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", patience=2, factor=0.5)

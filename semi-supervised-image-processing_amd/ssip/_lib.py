@@ -13,6 +13,23 @@ from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("SSIP_LIB", _HERE / "libssip_hip.so"))
+HEADER = _HERE.parents[1] / "include" / "ssip.h"
+
+
+def abi_version_expected() -> int:
+    """SSIP_ABI_VERSION as include/ssip.h declares it (the one source of truth
+    for build() and the tests).  Falls back to the compiled-in value of this
+    binding when the header is not shipped next to the package."""
+    import re
+
+    try:
+        m = re.search(r"^#define\s+SSIP_ABI_VERSION\s+(\d+)", HEADER.read_text(), re.M)
+    except OSError:
+        m = None
+    return int(m.group(1)) if m else ABI_VERSION
+
+
+ABI_VERSION = 4  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1
@@ -72,6 +89,7 @@ _SIGS = {
     "ssip_conv_wgrad_workspace_bytes": (_c_i64, [_PD]),
     "ssip_conv_wgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _vp]),
     "ssip_stem_bwd_wgrad_supported": (_c_int, [_PD, _c_int]),
+    "ssip_conv_kernel_name": (_c_int, [_c_int, _PD, _c_int, ctypes.c_char_p, _c_int]),
     "ssip_stem_bwd_wgrad": (_c_int, [_PD, _c_int] + [_vp] * 8 + [_c_int] * 3 + [_vp, _c_i64, _vp]),
     "ssip_bn_finalize": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_eval_coeffs": (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp, _vp]),

@@ -9,7 +9,9 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Optional
 
+import ctypes
 import os
+
 import torch
 
 from . import _lib
@@ -223,6 +225,13 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
         _timer.wrap("wgrad", g.flops(), call, *args)
         return
     call(*args)
+
+
+def conv_kernel_name(mode: str, g: ConvGeom, dtype: torch.dtype) -> str:
+    """The kernel ssip_conv_{fwd,dgrad,wgrad} selects for g (include/ssip.h)."""
+    buf = ctypes.create_string_buffer(160)
+    call("ssip_conv_kernel_name", {"fwd": 0, "dgrad": 1, "wgrad": 2}[mode], g.desc(), _DT[dtype], buf, 160)
+    return buf.value.decode()
 
 
 def stem_bwd_wgrad_supported(g: ConvGeom, dtype: torch.dtype) -> bool:

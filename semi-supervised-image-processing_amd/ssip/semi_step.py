@@ -115,6 +115,7 @@ class SemiStep:
         Bl = y_l.shape[0]
         out, dzl, dzs, pseudo, mask = ops.semi_loss(logits[:Bl].detach().contiguous(), y_l, zw.contiguous(),
                                                     logits[Bl:].detach().contiguous(), self.tau, self.lambda_u)
+        self.last = {"zw": zw, "logits": logits.detach(), "pseudo": pseudo, "mask": mask}  # device tensors
         logits.backward(torch.cat([dzl, dzs], 0))
         return out
 

@@ -18,7 +18,17 @@ def test_library_exports_every_symbol():
     lib = _lib.lib()
     for name in _lib.EXPORTED_SYMBOLS:
         assert hasattr(lib, name), name
-    assert lib.ssip_version() == 3
+    assert lib.ssip_version() == _lib.abi_version_expected() == _lib.ABI_VERSION
+
+
+def test_build_entry_checks_the_header_version():
+    # __graft_entry__.build() compares ssip_version() against the header's
+    # SSIP_ABI_VERSION (not a literal): both must agree with the built library
+    hdr = (ROOT / "include" / "ssip.h").read_text()
+    v = int(re.search(r"^#define\s+SSIP_ABI_VERSION\s+(\d+)", hdr, re.M).group(1))
+    assert _lib.abi_version_expected() == v == _lib.lib().ssip_version()
+    src = (ROOT / "__graft_entry__.py").read_text()
+    assert "abi_version_expected()" in src
 
 
 def test_argument_errors_surface_as_status_codes():

@@ -138,7 +138,7 @@ def test_cli_end_to_end(dev, tmp_path, monkeypatch):
     from src import supervised_training as T
 
     common = ["--strong-data-dir", str(data / "avec_labels"), "--batch-size", "4", "--num-workers", "0",
-              "--image-size", "64", "--target-recall", "0.9", "--min-precision", "0.5"]
+              "--image-size", "64", "--target-recall", "0.9", "--min-precision", "0.5", "--random-init"]
     T.main(common + ["--baseline-epochs", "1"])
     assert (tmp_path / "outputs/tables/results_comparison.csv").exists()
     assert (tmp_path / "outputs/models/baseline_resnet18.pt").exists()
@@ -153,8 +153,9 @@ def test_cli_end_to_end(dev, tmp_path, monkeypatch):
         assert (tmp_path / "outputs" / f).exists(), f
     sd = torch.load(tmp_path / "outputs/models/semi_resnet18.pt", weights_only=True)
     assert len(sd) == 122 and "layer4.1.bn2.running_var" in sd
-    FE.main(["--data-dir", str(data), "--batch-size", "8"])
+    FE.main(["--data-dir", str(data), "--batch-size", "8", "--random-init"])
     emb = np.load(tmp_path / "outputs/features/embeddings.npy")
     assert emb.shape == (36, 512) and emb.dtype == np.float32
     meta = json.loads((tmp_path / "outputs/features/metadata.json").read_text())
     assert meta["num_images"] == 36 and meta["embedding_dimension"] == 512
+    assert meta["weights"] == "random_init(seed=42)"

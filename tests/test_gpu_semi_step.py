@@ -113,3 +113,99 @@ def test_graph_replay_matches_eager(dev, dtype):
         assert torch.equal(a, b)
     # the run trained: the weights moved
     assert (we - w0).abs().max().item() > 1e-4
+
+
+def _rel_l2(a, b):
+    a = a.detach().double().cpu().flatten()
+    b = b.detach().double().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def test_semi_step_bf16_224_matches_oracle(dev):
+    """The benchmarked configuration's step in bf16 (224x224, 16 labelled +
+    16 unlabelled) against the float64 oracle on the same images and view
+    parameters.  Tolerances are DERIVED, per quantity, from a CPU run of the
+    same oracle with the engine's bf16 storage emulated (oracle/bf16_emulate:
+    bf16 conv inputs / weights / outputs and bf16 activation gradients):
+        weak logits      max-abs  <= max(2 * emulated, 1e-3 max|ref|)
+        losses           abs      <= max(3 * emulated, 2e-3 |ref|)
+        gradients        rel-L2   median <= max(2 * emulated median, 2e-2),
+                                  worst  <= max(3 * emulated worst, 2e-2)
+        running stats    max-abs  <= max(3 * emulated, 1e-3 max|ref|)
+    (per-tensor gradients of any bf16 implementation are far from fp64 at
+    random init -- ReLU-mask chaos, see tests/test_gpu_resnet.py -- so that
+    bound is statistical).  tau = 0.5 keeps every unlabelled sample (2
+    classes), so the strong-view gradients are exercised; the oracle uses the
+    device's pseudo-labels, which must equal its own argmax wherever the weak
+    logits are not within the tolerance of a tie."""
+    from oracle.bf16_emulate import emulate_bf16
+
+    S, Bl, Bu, tau, lr = 224, 16, 16, 0.5, 1e-4
+    rng = np.random.default_rng(5)
+    x_l = rng.integers(0, 256, (Bl, S, S, 3), dtype=np.uint8)
+    x_u = rng.integers(0, 256, (Bu, S, S, 3), dtype=np.uint8)
+    y_l = torch.from_numpy(rng.integers(0, 2, Bl))
+    g = torch.Generator().manual_seed(17)
+    dl = [draw_train_params(10.0, g) for _ in range(Bl)]
+    dw = [draw_train_params(10.0, g) for _ in range(Bu)]
+    ds = [draw_strong_params(S, g) for _ in range(Bu)]
+
+    torch.manual_seed(0)
+    ref = tvm.resnet18()
+    ref.fc = torch.nn.Linear(512, 2)
+    torch.manual_seed(0)
+    mine = replace_fc(SSIPResNet("resnet18", num_classes=1000, dtype="bf16"), 2).to(dev)
+    step = SemiStep(mine, lr=lr, weight_decay=1e-4, tau=tau, lambda_u=1.0, image_size=S)
+    params = (encode_params(dl, S, S), encode_params(dw, S, S), encode_params(ds, S, S))
+    st = step(torch.from_numpy(x_l).to(dev), y_l.to(dev), torch.from_numpy(x_u).to(dev), params)
+    torch.cuda.synchronize()
+    loss_gpu = st.loss.cpu().double()
+    zw_gpu = step.last["zw"].cpu().double()
+    pseudo_gpu = step.last["pseudo"].cpu()
+    named = dict(mine.named_parameters())
+    grads_gpu = {k: step.arena.grad_view(p).detach().cpu().double() for k, p in named.items()}
+    bufs_gpu = {k: b.detach().cpu() for k, b in mine.named_buffers()}
+
+    runs = {}
+    for kind in ("f64", "emu"):
+        m = copy.deepcopy(ref).double()
+        if kind == "emu":
+            emulate_bf16(m)
+        opt = torch.optim.AdamW(m.parameters(), lr=lr, weight_decay=1e-4)
+        aux = {}
+        out = semi_step_reference(m, opt, x_l, y_l, x_u, [_tuple(d) for d in dl], [_tuple(d) for d in dw],
+                                  [_tuple(d) for d in ds], S, tau, 1.0, pseudo_override=pseudo_gpu, out=aux)
+        runs[kind] = (out, aux, {k: p.grad.detach().clone() for k, p in m.named_parameters()},
+                      {k: b.detach().clone() for k, b in m.named_buffers()})
+    (l64, a64, g64, b64), (lem, aem, gem, bem) = runs["f64"], runs["emu"]
+
+    import statistics
+
+    zw_ref = a64["zw"]
+    tol_z = max(2 * (aem["zw"] - zw_ref).abs().max().item(), 1e-3 * zw_ref.abs().max().item())
+    err_z = (zw_gpu - zw_ref).abs().max().item()
+    print(f"weak logits: gpu {err_z:.3e} bound {tol_z:.3e}")
+    assert err_z <= tol_z
+    margin = (zw_ref[:, 0] - zw_ref[:, 1]).abs()
+    decided = margin > 2 * tol_z
+    assert torch.equal(pseudo_gpu[decided], zw_ref.argmax(1)[decided])
+    assert loss_gpu[3].item() == l64[3].item() == Bu
+    for i, name in enumerate(("total", "L_l", "L_u")):
+        tol = max(3 * abs(lem[i].item() - l64[i].item()), 2e-3 * abs(l64[i].item()))
+        err = abs(loss_gpu[i].item() - l64[i].item())
+        print(f"loss {name}: gpu {err:.3e} bound {tol:.3e}")
+        assert err <= tol, name
+    e_gpu = [_rel_l2(grads_gpu[k], g64[k]) for k in g64]
+    e_emu = [_rel_l2(gem[k], g64[k]) for k in g64]
+    med_g, med_e = statistics.median(e_gpu), statistics.median(e_emu)
+    print(f"gradient rel-L2: gpu median {med_g:.3e} worst {max(e_gpu):.3e}; "
+          f"emulated median {med_e:.3e} worst {max(e_emu):.3e}")
+    assert med_g <= max(2 * med_e, 2e-2)
+    assert max(e_gpu) <= max(3 * max(e_emu), 2e-2)
+    for k, b in b64.items():
+        if b.dtype.is_floating_point:
+            e_g = (bufs_gpu[k].double() - b).abs().max().item()
+            e_e = (bem[k] - b).abs().max().item()
+            assert e_g <= max(3 * e_e, 1e-3 * b.abs().max().item()), k
+        else:
+            assert torch.equal(bufs_gpu[k], b.cpu()), k

@@ -123,3 +123,29 @@ def test_transform_spec_rng_matches_torchvision_order():
 
     assert int(h.params[0]) == int(flip) and int(h.params[1]) == 1
     assert tuple(int(v) for v in h.params[2:8]) == rotate_fixed_point(angle, 224, 224)
+
+
+def test_create_model_without_weights_raises_unless_opted_in(monkeypatch):
+    """The reference's create_model downloads IMAGENET1K_V1 or fails
+    (common.py:299-304); offline, pretrained=True must fail the same way
+    unless the seeded random backbone is explicitly requested."""
+    from src.training.common import create_model
+
+    monkeypatch.delenv("SSIP_RESNET18_WEIGHTS", raising=False)
+    monkeypatch.delenv("SSIP_ALLOW_RANDOM_INIT", raising=False)
+    with pytest.raises(RuntimeError, match="random-init"):
+        create_model(2, pretrained=True)
+    m = create_model(2, pretrained=True, allow_random_init=True)
+    assert m.init_source == "random_init"
+    monkeypatch.setenv("SSIP_ALLOW_RANDOM_INIT", "1")
+    assert create_model(2, pretrained=True).init_source == "random_init"
+    assert create_model(2, pretrained=False).fc.out_features == 2
+
+
+def test_cli_random_init_flag():
+    from src import feature_extraction as FE
+    from src import semi_supervised_training as S
+
+    assert S.parse_args(["--strong-data-dir", "a", "--weak-data-dir", "b"]).random_init is False
+    assert S.parse_args(["--strong-data-dir", "a", "--weak-data-dir", "b", "--random-init"]).random_init is True
+    assert FE.parse_args(["--random-init"]).random_init is True

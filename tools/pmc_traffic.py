@@ -3,7 +3,10 @@ HBM section): FETCH_SIZE and WRITE_SIZE collected in SEPARATE runs (they do
 not fit one TCC pass); FETCH_SIZE doubled (gfx950 tallies 128-B requests at
 64 B); values are KiB per dispatch.
 
-usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json]
+usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json [workload-key]]
+(workload-key: bench.py's `_workload` string for the profiled command, e.g.
+"semi_consistency_resnet18_224 bs256 labeled128 bf16"; bench.py only reports
+the traffic of a file whose key matches its own run)
 Groups dispatches of the last complete step (between the last two AdamW
 launches) by kernel family and prints bytes per step.
 """
@@ -41,5 +44,7 @@ for k in sorted(set(fetch) | set(write)):
     wr = write.get(k, 0.0)
     out[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr}
     print(f"{k:12s} read {rd / 1e9:8.3f} GB  write {wr / 1e9:8.3f} GB  total {(rd + wr) / 1e9:8.3f} GB per step")
+if len(sys.argv) > 4:
+    out["_workload"] = sys.argv[4]
 if len(sys.argv) > 3:
     json.dump(out, open(sys.argv[3], "w"), indent=1)

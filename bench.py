@@ -58,11 +58,12 @@ def parse():
     ap.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet50"],
                     help="resnet50 + --image-size 512 --batch 128 = BASELINE config 5 (per GPU)")
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--graph", action="store_true",
-                    help="replay one captured hipGraph per step (default: eager launches, whose weak-forward and "
-                         "wgrad side streams overlap the main stream; HIP runs a graph's parallel branches one "
-                         "after another: 7.49 vs 7.15 ms/step measured)")
-    ap.add_argument("--eager", action="store_true", help="the default (kept for older command lines)")
+    ap.add_argument("--exec", dest="mode", default="eager", choices=["eager", "plan", "graph"],
+                    help="eager: Python enqueues every launch; plan: one step recorded, then replayed from C++ "
+                         "(ssip/plan.py, same streams and overlap); graph: one captured hipGraph per step (HIP runs "
+                         "a graph's parallel branches one after another)")
+    ap.add_argument("--graph", action="store_true", help="= --exec graph (older command lines)")
+    ap.add_argument("--eager", action="store_true", help="= --exec eager (older command lines)")
     return ap.parse_args()
 
 
@@ -91,8 +92,9 @@ def main():
             dist.broadcast(b, 0)
     bucketer = GradBucketer(model.flatten_parameters()) if world > 1 else None
     S = args.image_size
+    mode = "graph" if args.graph else "eager" if args.eager else args.mode
     step = SemiStep(model, lr=1e-4, weight_decay=1e-4, tau=0.7, image_size=S, bucketer=bucketer, seed=rank,
-                    graph=args.graph and not args.eager)
+                    graph=mode == "graph", plan=mode == "plan")
     step.overlap = not args.serial_weak
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
@@ -122,13 +124,16 @@ def main():
     # roofline leg: one instrumented step, HIP events around every conv launch
     timer = ops.ConvTimer()
     ops.set_conv_timer(timer)
-    graph, step.graph = step.graph, False  # the same kernels launched one by one, each bracketed by events
+    # the same kernels launched one by one from Python, each bracketed by events
+    graph, step.graph = step.graph, False
+    plan_mode, step.plan = step.plan, False
     # every launch on one stream: an event bracket must not include queueing
     # behind a kernel of another stream (weak forward, side-stream wgrads)
     side, resnet_mod.WGRAD_SIDE_STREAM = resnet_mod.WGRAD_SIDE_STREAM, False
     overlap, step.overlap = step.overlap, False
     step(x_l, y_l, x_u)
     step.graph = graph
+    step.plan = plan_mode
     step.overlap = overlap
     resnet_mod.WGRAD_SIDE_STREAM = side
     ops.set_conv_timer(None)

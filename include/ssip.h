@@ -245,6 +245,42 @@ typedef struct ssip_wprep {
 } ssip_wprep;
 int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* items, void* stream);
 
+/* num_batches_tracked += delta for `count` int64 device counters (the BN
+ * layers' num_batches_tracked, torch.nn.BatchNorm2d train-mode forward);
+ * ptrs is a HOST array of count <= SSIP_COUNTERS_MAX device pointers. */
+#define SSIP_COUNTERS_MAX 64
+int ssip_counters_add(int count, int64_t* const* ptrs, int64_t delta, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Launch plans: a recorded sequence of the stream-ordered entry points
+ * above, replayed from C++ (the host-side counterpart of a hipGraph that
+ * keeps multi-stream concurrency: HIP executes a graph's parallel branches
+ * one after another).  The Python engine records one step while running it
+ * (ssip/plan.py); a replay then enqueues the same launches, with the same
+ * device pointers, on the same streams, with no Python in the loop.
+ *   - a call records the function (index from ssip_plan_fn_index) and one
+ *     64-bit slot per argument: integers and device pointers as their value,
+ *     floats as their bit pattern; an argument with blob_len[i] > 0 is a HOST
+ *     pointer to blob_len[i] bytes, copied into the plan at record time (conv
+ *     descriptors, weight-prep tables, mean/std triples, counter tables);
+ *   - events order streams: ssip_plan_add_event records an event on a stream,
+ *     ssip_plan_add_wait makes another stream wait for it;
+ *   - markers cut the plan into segments so the caller can run host work
+ *     (collective launches) between them: ssip_plan_run(plan, seg).
+ * Only functions whose last parameter is the stream can be recorded. */
+typedef struct ssip_plan ssip_plan;
+ssip_plan* ssip_plan_create(void);
+void ssip_plan_destroy(ssip_plan* plan);
+int ssip_plan_fn_index(const char* name);
+int ssip_plan_add_call(ssip_plan* plan, int fn, int nargs, const uint64_t* slots, const int64_t* blob_len,
+                       const void* blob_data);
+int ssip_plan_add_event(ssip_plan* plan, void* stream);
+int ssip_plan_add_wait(ssip_plan* plan, void* stream, int event);
+int ssip_plan_add_marker(ssip_plan* plan);
+int ssip_plan_segments(const ssip_plan* plan);
+int64_t ssip_plan_num_ops(const ssip_plan* plan);
+int ssip_plan_run(ssip_plan* plan, int segment);
+
 #ifdef __cplusplus
 }
 #endif

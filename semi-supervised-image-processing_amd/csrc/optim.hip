@@ -209,3 +209,30 @@ extern "C" int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* it
   });
   return ::ssip::check_launch("weight_prep_batch");
 }
+
+// ---------------------------------------------------------------------------
+// BatchNorm num_batches_tracked += delta for every BN layer in one launch
+// ---------------------------------------------------------------------------
+namespace {
+struct CounterTable {
+  int64_t* p[SSIP_COUNTERS_MAX];
+};
+
+__global__ void counters_add_kernel(CounterTable t, int count, int64_t delta) {
+  const int i = threadIdx.x;
+  if (i < count) t.p[i][0] += delta;
+}
+}  // namespace
+
+extern "C" int ssip_counters_add(int count, int64_t* const* ptrs, int64_t delta, void* stream) {
+  SSIP_REQUIRE(count >= 0 && count <= SSIP_COUNTERS_MAX && (count == 0 || ptrs), SSIP_ERR_ARG,
+               "ssip_counters_add: count must be 0..%d", SSIP_COUNTERS_MAX);
+  if (count == 0) return SSIP_OK;
+  CounterTable t;
+  for (int i = 0; i < count; ++i) {
+    SSIP_REQUIRE(ptrs[i], SSIP_ERR_ARG, "ssip_counters_add: null counter %d", i);
+    t.p[i] = ptrs[i];
+  }
+  hipLaunchKernelGGL(counters_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t, count, delta);
+  return ::ssip::check_launch("counters_add");
+}

@@ -1,0 +1,181 @@
+// Launch plans (include/ssip.h "Launch plans"): a recorded sequence of the
+// library's stream-ordered entry points, replayed from C++.
+//
+// Why: one eager train step is ~250 launches; enqueued from Python each costs
+// ~25 us of interpreter + ctypes + allocator work (the step was within ~10 %
+// of being host-bound).  A hipGraph removes that cost but HIP runs a graph's
+// parallel branches one after another, which loses the weak-forward and
+// side-stream wgrad overlap.  A plan keeps both: replay is a tight C++ loop
+// over typed calls with fixed pointers, and cross-stream order is kept with
+// the same event record / wait pairs the eager step uses.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <memory>
+#include <vector>
+
+#include "../../include/ssip.h"
+
+namespace ssip {
+void set_error(const char* fmt, ...);
+}
+
+namespace {
+
+inline float plan_f32(uint64_t v) {
+  uint32_t u = (uint32_t)v;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+inline double plan_f64(uint64_t v) {
+  double d;
+  memcpy(&d, &v, 8);
+  return d;
+}
+
+struct PlanFn {
+  const char* name;
+  int nargs;
+  int (*call)(const uint64_t* a);
+};
+
+#include "plan_thunks.inc"
+
+constexpr int kNumFns = (int)(sizeof(kPlanFns) / sizeof(kPlanFns[0]));
+
+enum OpKind { OP_CALL = 0, OP_EVENT = 1, OP_WAIT = 2, OP_MARK = 3 };
+
+struct Op {
+  int kind;
+  int fn;          // OP_CALL
+  int64_t arg0;    // OP_CALL: first slot in Plan::slots
+  int event;       // OP_EVENT / OP_WAIT
+  hipStream_t stream;
+};
+
+}  // namespace
+
+struct ssip_plan {
+  std::vector<Op> ops;
+  std::vector<uint64_t> slots;
+  std::vector<std::unique_ptr<uint8_t[]>> blobs;
+  std::vector<hipEvent_t> events;
+  std::vector<size_t> seg_begin{0};  // op index where each segment starts
+  ~ssip_plan() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+  }
+};
+
+extern "C" {
+
+ssip_plan* ssip_plan_create(void) { return new (std::nothrow) ssip_plan(); }
+
+void ssip_plan_destroy(ssip_plan* plan) { delete plan; }
+
+int ssip_plan_fn_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < kNumFns; ++i)
+    if (strcmp(kPlanFns[i].name, name) == 0) return i;
+  return -1;
+}
+
+int ssip_plan_add_call(ssip_plan* plan, int fn, int nargs, const uint64_t* slots, const int64_t* blob_len,
+                       const void* blob_data) {
+  if (!plan || fn < 0 || fn >= kNumFns || nargs != kPlanFns[fn].nargs || (nargs && !slots)) {
+    ::ssip::set_error("ssip_plan_add_call: bad plan, function index %d or argument count %d", fn, nargs);
+    return SSIP_ERR_ARG;
+  }
+  Op op{OP_CALL, fn, (int64_t)plan->slots.size(), -1, nullptr};
+  const uint8_t* bd = static_cast<const uint8_t*>(blob_data);
+  for (int i = 0; i < nargs; ++i) {
+    uint64_t v = slots[i];
+    if (blob_len && blob_len[i] > 0) {
+      if (!bd) {
+        ::ssip::set_error("ssip_plan_add_call: blob argument %d without data", i);
+        return SSIP_ERR_ARG;
+      }
+      std::unique_ptr<uint8_t[]> b(new (std::nothrow) uint8_t[blob_len[i]]);
+      if (!b) {
+        ::ssip::set_error("ssip_plan_add_call: out of host memory");
+        return SSIP_ERR_ARG;
+      }
+      memcpy(b.get(), bd, (size_t)blob_len[i]);
+      bd += blob_len[i];
+      v = (uint64_t)(uintptr_t)b.get();
+      plan->blobs.push_back(std::move(b));
+    }
+    plan->slots.push_back(v);
+  }
+  plan->ops.push_back(op);
+  return SSIP_OK;
+}
+
+int ssip_plan_add_event(ssip_plan* plan, void* stream) {
+  if (!plan) return SSIP_ERR_ARG;
+  hipEvent_t e;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    ::ssip::set_error("ssip_plan_add_event: hipEventCreateWithFlags failed");
+    return SSIP_ERR_LAUNCH;
+  }
+  plan->events.push_back(e);
+  const int id = (int)plan->events.size() - 1;
+  plan->ops.push_back(Op{OP_EVENT, -1, 0, id, (hipStream_t)stream});
+  return id;
+}
+
+int ssip_plan_add_wait(ssip_plan* plan, void* stream, int event) {
+  if (!plan || event < 0 || event >= (int)plan->events.size()) {
+    ::ssip::set_error("ssip_plan_add_wait: unknown event %d", event);
+    return SSIP_ERR_ARG;
+  }
+  plan->ops.push_back(Op{OP_WAIT, -1, 0, event, (hipStream_t)stream});
+  return SSIP_OK;
+}
+
+int ssip_plan_add_marker(ssip_plan* plan) {
+  if (!plan) return SSIP_ERR_ARG;
+  plan->seg_begin.push_back(plan->ops.size());
+  return (int)plan->seg_begin.size() - 1;
+}
+
+int ssip_plan_segments(const ssip_plan* plan) { return plan ? (int)plan->seg_begin.size() : -1; }
+
+int64_t ssip_plan_num_ops(const ssip_plan* plan) { return plan ? (int64_t)plan->ops.size() : -1; }
+
+int ssip_plan_run(ssip_plan* plan, int segment) {
+  if (!plan || segment < 0 || segment >= (int)plan->seg_begin.size()) {
+    ::ssip::set_error("ssip_plan_run: bad plan or segment %d", segment);
+    return SSIP_ERR_ARG;
+  }
+  const size_t b = plan->seg_begin[segment];
+  const size_t e = segment + 1 < (int)plan->seg_begin.size() ? plan->seg_begin[segment + 1] : plan->ops.size();
+  for (size_t i = b; i < e; ++i) {
+    const Op& op = plan->ops[i];
+    switch (op.kind) {
+      case OP_CALL: {
+        const int rc = kPlanFns[op.fn].call(plan->slots.data() + op.arg0);
+        if (rc != SSIP_OK) return rc;  // the entry point set the message
+        break;
+      }
+      case OP_EVENT:
+        if (hipEventRecord(plan->events[op.event], op.stream) != hipSuccess) {
+          ::ssip::set_error("ssip_plan_run: hipEventRecord failed at op %zu", i);
+          return SSIP_ERR_LAUNCH;
+        }
+        break;
+      case OP_WAIT:
+        if (hipStreamWaitEvent(op.stream, plan->events[op.event], 0) != hipSuccess) {
+          ::ssip::set_error("ssip_plan_run: hipStreamWaitEvent failed at op %zu", i);
+          return SSIP_ERR_LAUNCH;
+        }
+        break;
+      default:
+        break;
+    }
+  }
+  return SSIP_OK;
+}
+
+}  // extern "C"

@@ -120,6 +120,18 @@ _SIGS = {
     "ssip_adamw_dev": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _vp]),
     "ssip_weight_prep": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp, _vp]),
     "ssip_weight_prep_batch": (_c_int, [_c_int, _c_int, ctypes.POINTER(WPrep), _vp]),
+    "ssip_counters_add": (_c_int, [_c_int, _vp, _c_i64, _vp]),
+    # launch plans (ssip/plan.py)
+    "ssip_plan_create": (_vp, []),
+    "ssip_plan_destroy": (None, [_vp]),
+    "ssip_plan_fn_index": (_c_int, [ctypes.c_char_p]),
+    "ssip_plan_add_call": (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp]),
+    "ssip_plan_add_event": (_c_int, [_vp, _vp]),
+    "ssip_plan_add_wait": (_c_int, [_vp, _vp, _c_int]),
+    "ssip_plan_add_marker": (_c_int, [_vp]),
+    "ssip_plan_segments": (_c_int, [_vp]),
+    "ssip_plan_num_ops": (_c_i64, [_vp]),
+    "ssip_plan_run": (_c_int, [_vp, _c_int]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -153,7 +165,12 @@ def check(rc: int, what: str) -> None:
 
 # int-returning queries (not status codes)
 _NOT_STATUS = ("ssip_version", "ssip_conv_fwd_partial_tiles", "ssip_conv_dgrad_bn_partial_tiles",
-               "ssip_stem_bwd_wgrad_supported")
+               "ssip_stem_bwd_wgrad_supported", "ssip_plan_fn_index", "ssip_plan_segments")
+
+# Active launch-plan recorder (ssip.plan.PlanRecorder) or None.  While set,
+# every stream-ordered call made through `call` is also appended to the plan,
+# and every tensor whose pointer is taken through `ptr` is kept alive by it.
+RECORDER = None
 
 
 def call(name: str, *args) -> int:
@@ -161,4 +178,13 @@ def call(name: str, *args) -> int:
     rc = fn(*args)
     if _SIGS[name][0] is _c_int and name not in _NOT_STATUS:
         check(rc, name)
+    if RECORDER is not None:
+        RECORDER.on_call(name, args)
     return rc
+
+
+def ptr(t) -> int:
+    """Device pointer of tensor t (kept alive by an active recorder)."""
+    if RECORDER is not None:
+        RECORDER.keep.append(t)
+    return t.data_ptr()

@@ -192,8 +192,9 @@ class GpuTransform:
 
         self._mean_arr = (ctypes.c_float * 3)(*[float(v) for v in mean])
         self._std_arr = (ctypes.c_float * 3)(*[float(v) for v in std])
-        self.mean = ctypes.addressof(self._mean_arr)
-        self.std = ctypes.addressof(self._std_arr)
+        # passed as the ctypes arrays (host pointers): a launch plan copies them
+        self.mean = self._mean_arr
+        self.std = self._std_arr
         self._tables: Dict[Tuple[int, int, str], Tuple[torch.Tensor, torch.Tensor, int]] = {}
 
     def _table(self, n_in: int, n_out: int, dev) -> Tuple[torch.Tensor, torch.Tensor, int]:
@@ -233,8 +234,8 @@ class GpuTransform:
         if Wr != W:
             bh, ch, kh = self._table(W, Wr, dev)
             tmp = torch.empty((B, H, Wr, 3), device=dev, dtype=torch.uint8)
-            _lib.call("ssip_resize_h_u8", B, images.data_ptr(), bstride, H, W, Wr, kh, bh.data_ptr(), ch.data_ptr(),
-                      tmp.data_ptr(), stream)
+            _lib.call("ssip_resize_h_u8", B, _lib.ptr(images), bstride, H, W, Wr, kh, _lib.ptr(bh), _lib.ptr(ch),
+                      _lib.ptr(tmp), stream)
             src, src_w, bstride = tmp, Wr, H * Wr * 3
         kv, bv, cv = 0, None, None
         if Hr != H:
@@ -249,10 +250,10 @@ class GpuTransform:
         if params is not None:
             params = params.to(dev, torch.int32).contiguous()
             assert params.shape == (B, PARAM_FIELDS)
-            pptr = params.data_ptr()
-        _lib.call("ssip_augment_u8", _lib.F32 if self.dtype == torch.float32 else _lib.BF16, B, src.data_ptr(),
-                  bstride, src_h, src_w, Hr, Wr, Ho, Wo, cx, cy, kv, None if bv is None else bv.data_ptr(),
-                  None if cv is None else cv.data_ptr(), pptr, self.mean, self.std, p, out.data_ptr(), stream)
+            pptr = _lib.ptr(params)
+        _lib.call("ssip_augment_u8", _lib.F32 if self.dtype == torch.float32 else _lib.BF16, B, _lib.ptr(src),
+                  bstride, src_h, src_w, Hr, Wr, Ho, Wo, cx, cy, kv, None if bv is None else _lib.ptr(bv),
+                  None if cv is None else _lib.ptr(cv), pptr, self.mean, self.std, p, _lib.ptr(out), stream)
         return DeviceImages(out, p)
 
 

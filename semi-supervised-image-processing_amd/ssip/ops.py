@@ -34,13 +34,45 @@ def _p(t: Optional[torch.Tensor]):
         raise ValueError("ssip: tensor must be on the HIP device")
     if not t.is_contiguous():
         raise ValueError("ssip: tensor must be contiguous")
-    return t.data_ptr()
+    return _lib.ptr(t)
 
 
 def stream_ptr() -> int:
     """Raw hipStream_t of the calling thread's current stream (the plain
     torch.cuda.current_stream() path costs ~8 us per call; a step makes ~130)."""
     return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+
+
+def wait_stream(dst: "torch.cuda.Stream", src: "torch.cuda.Stream") -> None:
+    """dst waits for the work enqueued on src so far (torch's wait_stream);
+    recorded into an active launch plan as an event record / wait pair."""
+    dst.wait_stream(src)
+    r = _lib.RECORDER
+    if r is not None:
+        r.wait_stream(dst.cuda_stream, src.cuda_stream)
+
+
+def host_callback(fn, *args):
+    """Run host work that issues device work outside the C ABI (collectives).
+    Inside a launch-plan recording this ends a plan segment and is re-run at
+    that point of every replay (its own launches are not recorded)."""
+    r = _lib.RECORDER
+    if r is None:
+        return fn(*args)
+    r.callback(fn, args)
+    _lib.RECORDER = None
+    try:
+        return fn(*args)
+    finally:
+        _lib.RECORDER = r
+
+
+def counters_add(counters, delta: int = 1) -> None:
+    """tensor += delta for a list of int64 one-element device tensors, one launch."""
+    for i in range(0, len(counters), 64):
+        chunk = counters[i:i + 64]
+        arr = (ctypes.c_void_p * len(chunk))(*[_p(t) for t in chunk])
+        call("ssip_counters_add", len(chunk), arr, int(delta), stream_ptr())
 
 
 # ---------------------------------------------------------------------------
@@ -372,14 +404,21 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, grad_scale: float 
     return loss, dl, pred
 
 
-def semi_loss(zl, yl, zw, zs, tau: float, lambda_u: float):
+def semi_loss(zl, yl, zw, zs, tau: float, lambda_u: float, dz: Optional[torch.Tensor] = None):
+    """dz (optional): one [Bl+Bu, J] buffer receiving [dzl; dzs] (the joint
+    forward's logit gradient, written in place: no concatenation pass)."""
     Bl = 0 if zl is None else zl.shape[0]
     Bu = 0 if zw is None else zw.shape[0]
     J = (zl if zl is not None else zw).shape[1]
     dev = (zl if zl is not None else zw).device
     out = torch.empty(4, device=dev, dtype=torch.float32)
-    dzl = torch.empty_like(zl) if zl is not None else None
-    dzs = torch.empty_like(zs) if zs is not None else None
+    if dz is not None:
+        assert dz.shape == (Bl + Bu, J) and dz.dtype == torch.float32 and dz.is_contiguous()
+        dzl = dz[:Bl] if zl is not None else None
+        dzs = dz[Bl:] if zs is not None else None
+    else:
+        dzl = torch.empty_like(zl) if zl is not None else None
+        dzs = torch.empty_like(zs) if zs is not None else None
     pseudo = torch.empty(Bu, device=dev, dtype=torch.int64) if Bu else None
     mask = torch.empty(Bu, device=dev, dtype=torch.uint8) if Bu else None
     call("ssip_semi_loss", Bl, Bu, J, _p(zl), _p(yl), _p(zw), _p(zs), float(tau), float(lambda_u), _p(out), _p(dzl),

@@ -438,12 +438,16 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
 
 
 def _bump_batches_tracked(model: SSIPResNet):
+    """num_batches_tracked += 1 on every BN layer (torch's train-mode BN), one launch."""
     t = getattr(model, "_nbt", None)
-    if t is None:
+    if t is None or (t and t[0].device != model.conv1.weight.device):
         t = [m.num_batches_tracked for m in model.modules()
              if isinstance(m, nn.BatchNorm2d) and m.num_batches_tracked is not None]
         model._nbt = t
-    torch._foreach_add_(t, 1)
+    if t and t[0].is_cuda:
+        ops.counters_add(t, 1)
+    else:
+        torch._foreach_add_(t, 1)
 
 
 # ---------------------------------------------------------------------------
@@ -501,7 +505,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     try:
         _backward_impl(model, sv, dlogits, main, side)
     finally:
-        main.wait_stream(side)
+        ops.wait_stream(main, side)
 
 
 def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, side):
@@ -523,14 +527,20 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     if fc.bias is not None and fc.bias.requires_grad:
         db, accb = _grad_target(fc.bias, arena)
     user_hook = getattr(model, "grad_ready_hook", None)
-    hook = user_hook
-    if user_hook is not None and side is not None:
+    hook = None
+    if user_hook is not None and side is None:
         def hook(params):
+            ops.host_callback(user_hook, params)
+    elif user_hook is not None:
+        def _on_side(params):
             # the hook's consumers (gradient buckets) order themselves after
             # the current stream: make that the side stream, joined to main
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 user_hook(params)
+
+        def hook(params):
+            ops.host_callback(_on_side, params)
     if not trunk_trainable:
         if dw is not None:
             ops.avgpool_fc_bwd(dt, N, sv.last_pq, C, J, dlogits, fc_w.detach(), sv.feat, None, dw,
@@ -615,7 +625,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         if side is None:
             ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
             return
-        side.wait_stream(main)
+        ops.wait_stream(side, main)
         with torch.cuda.stream(side):
             ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
         dy.record_stream(side)
@@ -714,7 +724,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         if side is None:
             ops.stem_bwd_wgrad(*args)
         else:
-            side.wait_stream(main)
+            ops.wait_stream(side, main)
             with torch.cuda.stream(side):
                 ops.stem_bwd_wgrad(*args)
             for t in (dz, coef1):

@@ -54,7 +54,7 @@ class SemiStep:
 
     def __init__(self, model: SSIPResNet, lr: float = 1e-4, weight_decay: float = 1e-4, tau: float = 0.7,
                  lambda_u: float = 1.0, image_size: int = 224, bucketer=None, seed: int = 0, graph: bool = False,
-                 eager_warmup: int = 2):
+                 eager_warmup: int = 2, plan: bool = False):
         self.model = model
         self.arena = model.flatten_parameters()
         self.opt = AdamW(model.parameters(), lr=lr, weight_decay=weight_decay, arena=self.arena)
@@ -71,7 +71,11 @@ class SemiStep:
         self.eager_warmup = eager_warmup
         self._calls = 0
         self._g = None
-        if graph:
+        if graph and plan:
+            raise ValueError("SemiStep: graph and plan are alternatives")
+        self.plan = plan
+        self._plan = None
+        if graph or plan:
             self.opt.use_device_schedule()
 
     def _side_stream(self, dev):
@@ -113,10 +117,11 @@ class SemiStep:
     def _loss_bwd(self, logits, y_l, zw) -> torch.Tensor:
         """loss + dlogits in one launch, then the backward."""
         Bl = y_l.shape[0]
+        dz = torch.empty_like(logits, dtype=torch.float32)
         out, dzl, dzs, pseudo, mask = ops.semi_loss(logits[:Bl].detach().contiguous(), y_l, zw.contiguous(),
-                                                    logits[Bl:].detach().contiguous(), self.tau, self.lambda_u)
+                                                    logits[Bl:].detach().contiguous(), self.tau, self.lambda_u, dz=dz)
         self.last = {"zw": zw, "logits": logits.detach(), "pseudo": pseudo, "mask": mask}  # device tensors
-        logits.backward(torch.cat([dzl, dzs], 0))
+        logits.backward(dz)
         return out
 
     def _fwd_bwd(self, x_l, y_l, x_u, pl, pw, ps) -> torch.Tensor:
@@ -129,12 +134,13 @@ class SemiStep:
         # compute-dtype weights for both forwards, refreshed once, before the fork
         m.prepare_weights(need_t=True)
         side = self._side_stream(dev) if self.overlap else main
-        side.wait_stream(main)
+        if side is not main:
+            ops.wait_stream(side, main)
         with torch.cuda.stream(side):
             zw = self._weak(x_u, pw)
         logits = self._train_fwd(x_l, x_u, pl, ps)
         if side is not main:
-            main.wait_stream(side)
+            ops.wait_stream(main, side)
             zw.record_stream(main)
         return self._loss_bwd(logits, y_l, zw)
 
@@ -147,12 +153,51 @@ class SemiStep:
         self._calls += 1
         if self.graph and self._calls > self.eager_warmup:
             return self._replay(x_l, y_l, x_u, params)
+        if self.plan and self._calls > self.eager_warmup:
+            return self._plan_step(x_l, y_l, x_u, params)
         pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
         out = self._fwd_bwd(x_l, y_l, x_u, pl, pw, ps)
         scale = self.bucketer.finish() if self.bucketer is not None else 1.0
         # 6. optimizer
         self.opt.step(grad_scale=scale)
         return StepStats(loss=out)
+
+    # ------------------------------------------------------------------
+    # launch-plan path (ssip/plan.py): record one step, replay it from C++
+    # ------------------------------------------------------------------
+    def _finish_buckets(self):
+        self.bucketer.finish()
+
+    def _plan_step(self, x_l, y_l, x_u, params) -> StepStats:
+        """Steps 1-6 replayed from the recorded plan: the same launches on the
+        same streams (weak forward and wgrads still overlap), with the gradient
+        buckets' all-reduces launched between plan segments."""
+        from torch.autograd.graph import increment_version
+
+        from .plan import Plan
+
+        dev = x_l.device
+        if self._plan is None:
+            self._static = (x_l.clone(), y_l.clone(), x_u.clone()) + tuple(p.to(dev) for p in params)
+            plan = Plan()
+            scale = 1.0 / self.bucketer.world if self.bucketer is not None else 1.0
+            with plan:
+                out = self._fwd_bwd(*self._static)
+                if self.bucketer is not None:
+                    ops.host_callback(self._finish_buckets)
+                self.opt.step(grad_scale=scale)
+            self._plan, self._plan_out = plan, out
+            return StepStats(loss=out)
+        for dst, src in zip(self._static, (x_l, y_l, x_u) + tuple(params)):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        if self.bucketer is not None:
+            self.bucketer.reset()
+        self._plan.replay()
+        # the replay's AdamW changed the weights behind torch's back: bump the
+        # versions so an eager forward afterwards refreshes its weight copies
+        increment_version(list(self.model.parameters()))
+        return StepStats(loss=self._plan_out)
 
     # ------------------------------------------------------------------
     # hipGraph path

@@ -82,6 +82,43 @@ def test_semi_step_matches_oracle(dev, overlap):
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_plan_replay_matches_eager(dev, dtype, overlap):
+    """SemiStep(plan=True) -- 2 eager steps, one recorded step, replays from
+    C++ (csrc/plan.cpp) -- gives the same losses, weights and BN buffers, bit
+    for bit, as the eager step with the device-side AdamW schedule: the
+    launches, their order and their streams are identical."""
+    S, Bl, Bu = 64, 8, 8
+    g = torch.Generator().manual_seed(4)
+    x_l = torch.randint(0, 256, (Bl, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    x_u = torch.randint(0, 256, (Bu, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    y_l = torch.randint(0, 2, (Bl,), generator=g).to(dev)
+    runs = []
+    for plan in (False, True):
+        torch.manual_seed(0)
+        m = replace_fc(SSIPResNet("resnet18", 1000, dtype=dtype), 2).to(dev).train()
+        step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=S, seed=11, plan=plan)
+        step.overlap = overlap
+        step.opt.use_device_schedule()
+        w0 = step.arena.flat.detach().cpu().clone()
+        losses = []
+        for _ in range(6):
+            losses.append(step(x_l, y_l, x_u).loss.clone())
+        torch.cuda.synchronize()
+        if plan:
+            assert step._plan is not None and step._plan.num_ops > 100
+        runs.append((torch.stack(losses).cpu(), step.arena.flat.detach().cpu().clone(),
+                     step.opt.device_step_count(), [b.detach().cpu().clone() for b in m.buffers()]))
+    (le, we, te, be), (lp, wp, tp, bp) = runs
+    assert te == tp == 6
+    assert torch.equal(le, lp), (le, lp)
+    assert torch.equal(we, wp)
+    for a, b in zip(be, bp):
+        assert torch.equal(a, b)
+    assert (we - w0).abs().max().item() > 1e-4
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_graph_replay_matches_eager(dev, dtype):
     """SemiStep(graph=True) — 2 eager steps, capture, replays — produces the
     same losses and the same weights, bit for bit, as the eager step with the

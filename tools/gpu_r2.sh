@@ -9,6 +9,7 @@ cd "$R"
 export TMPDIR=/tmp
 out=gpurun_out/$tag
 mkdir -p $out
+nb=0
 for st in "$@"; do
   case $st in
     tests|tests:*)
@@ -19,9 +20,9 @@ for st in "$@"; do
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc   # 1 = test failures (keep going), else abort
       ;;
     bench|bench:*)
-      a=${st#bench}; a=${a#:}
-      timeout -k 10 420 python bench.py $a > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
-      tail -1 $out/bench.log
+      a=${st#bench}; a=${a#:}; nb=$((nb+1))
+      timeout -k 10 420 python bench.py $a > $out/bench$nb.log 2>&1 || { tail -20 $out/bench$nb.log; exit 1; }
+      tail -1 $out/bench$nb.log
       ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
@@ -39,6 +40,12 @@ for st in "$@"; do
       timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $out/$c -o run -- \
         python bench.py --steps 3 --warmup 3 --no-cpu-baseline > $out/$c.log 2>&1 || { tail -20 $out/$c.log; exit 1; }
       tail -1 $out/$c.log
+      ;;
+    py:*)
+      # an arbitrary python tool: py:<script> [args] (timeout 300)
+      c=${st#py:}
+      timeout -k 10 300 python $c > $out/py_$(basename ${c%% *} .py).log 2>&1 || { tail -20 $out/py_$(basename ${c%% *} .py).log; exit 1; }
+      tail -5 $out/py_$(basename ${c%% *} .py).log
       ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

@@ -45,6 +45,11 @@ def base_parser(doc: str, weak_required: bool) -> argparse.ArgumentParser:
     if weak_required:
         p.add_argument("--unlabeled-cohort-csv", type=Path, default=None,
                        help="Optional CSV listing unlabeled image paths to include in pseudo-labeling (column: path).")
+        p.add_argument("--consistency", action="store_true",
+                       help="Replace the frozen-backbone pseudo-label pretrain with joint consistency training "
+                            "(labelled CE + lambda * masked CE of strong views on weak-view pseudo-labels, "
+                            "--pseudo-threshold as tau) for --weak-pretrain-epochs epochs (BASELINE config 3).")
+        p.add_argument("--lambda-u", type=float, default=1.0, help="Consistency-loss weight (--consistency).")
     # ssip extensions (optional)
     p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"],
                    help="Activation dtype of the HIP kernels (fp32 = reference numerics, bf16 = throughput).")
@@ -79,4 +84,6 @@ def to_config(a, semi: bool) -> TrainingConfig:
         semi_checkpoint=o / "models/semi_resnet18.pt",
         unlabeled_cohort_csv=a.unlabeled_cohort_csv if semi else None,
         dtype=a.dtype, weights=a.weights, random_init=a.random_init,
+        consistency=bool(getattr(a, "consistency", False)) if semi else False,
+        lambda_u=float(getattr(a, "lambda_u", 1.0)),
     )

@@ -33,6 +33,8 @@ _PKG = Path(__file__).resolve().parents[1]
 if str(_PKG) not in sys.path:
     sys.path.insert(0, str(_PKG))
 
+from ssip.dist import shard_range  # noqa: E402
+from .training import distributed as D  # noqa: E402
 from ssip import SSIPResNet  # noqa: E402
 from ssip.augment import GpuTransform  # noqa: E402
 
@@ -184,8 +186,15 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
         except (UnidentifiedImageError, OSError) as exc:
             return rec, None, exc
 
+    # data parallel (torchrun): this rank's contiguous run of whole batches; the
+    # per-batch results are gathered in rank order = the single-process order
+    mine = records
+    if D.world() > 1:
+        nb = (len(records) + batch_size - 1) // batch_size
+        blo, bhi = shard_range(nb, D.rank(), D.world())
+        mine = records[blo * batch_size:min(bhi * batch_size, len(records))]
     with ThreadPoolExecutor(max_workers=decode_threads) as pool:
-        for chunk in batched(records, batch_size):
+        for chunk in batched(mine, batch_size):
             t0 = time.perf_counter()
             ok_recs, arrays = [], []
             for rec, arr, exc in pool.map(decode, chunk):
@@ -207,6 +216,8 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
             kept.extend(ok_recs)
             per = (time.perf_counter() - t0) / len(ok_recs)
             times.extend([per] * len(ok_recs))
+    if D.world() > 1:
+        embeddings, kept, failures, times = (D.gather_list(v) for v in (embeddings, kept, failures, times))
     if not embeddings:
         raise RuntimeError("No embeddings were generated; all images failed to decode?")
     mat = np.concatenate(embeddings, 0)
@@ -332,6 +343,7 @@ def main(argv=None) -> None:
     device = torch.device(args.device)
     if device.type != "cuda":
         raise RuntimeError("ssip feature extraction runs on the HIP device (--device cuda)")
+    device = D.setup(device)  # torchrun: one rank per GPU, file list sharded by batch
     logging.info("Starting feature extraction on device %s", device)
     records = discover_image_records(args.data_dir)
     t0 = time.perf_counter()
@@ -340,8 +352,9 @@ def main(argv=None) -> None:
     logging.info("Completed embedding extraction in %.2f seconds", time.perf_counter() - t0)
     stats = run_sanity_checks(res.embeddings)
     probe = nearest_neighbor_probe(res.embeddings, res.records)
-    save_artifacts(res, stats, probe, args.data_dir, device)
-    logging.info("Artifacts saved to %s", FEATURE_OUTPUT_DIR)
+    if D.is_main():
+        save_artifacts(res, stats, probe, args.data_dir, device)
+        logging.info("Artifacts saved to %s", FEATURE_OUTPUT_DIR)
 
 
 if __name__ == "__main__":

@@ -53,6 +53,8 @@ from ssip.data import Collate, DeviceTransformSpec, ImageFolder, pil_loader  # n
 from ssip.optim import AdamW  # noqa: E402
 from ssip.resnet import DeviceImages  # noqa: E402
 
+from . import distributed as D  # noqa: E402
+
 LOGGER = logging.getLogger(__name__)
 
 # ---------------------------------------------------------------------------
@@ -100,6 +102,8 @@ class TrainingConfig:
     dtype: str = "fp32"
     weights: Optional[Path] = None
     random_init: bool = False   # opt in to the seeded random backbone when no ImageNet weights are local
+    consistency: bool = False   # semi stage = joint weak/strong consistency training (ssip.semi_step.SemiStep)
+    lambda_u: float = 1.0       # weight of the unlabelled consistency term (--consistency)
 
 
 # ---------------------------------------------------------------------------
@@ -128,11 +132,11 @@ def resolve_device(device: str) -> torch.device:
     if device == "auto":
         if not torch.cuda.is_available():
             raise RuntimeError("ssip: no HIP device visible; this framework runs its compute on MI355X only")
-        return torch.device("cuda")
+        return D.setup(torch.device("cuda"))
     if device == "cpu":
         raise RuntimeError("ssip: --device cpu is not supported (the compute path is the HIP kernels); "
                            "use --device cuda or auto")
-    return torch.device(device)
+    return D.setup(torch.device(device))
 
 
 # ---------------------------------------------------------------------------
@@ -232,6 +236,8 @@ def prepare_dataloaders(strong_data_dir: Path, transforms_map, batch_size: int, 
     val_ds = TransformSubset(base, list(va), transform=transforms_map["eval"], return_paths=True)
     test_ds = TransformSubset(base, list(te), transform=transforms_map["eval"], return_paths=True)
     sampler = make_balanced_sampler(targets[tr].tolist())
+    if D.world() > 1:  # the same global draw on every rank, rank-strided
+        sampler = D.RankStridedSampler(sampler)
     return (_loader(train_ds, transforms_map["train"], batch_size, num_workers, sampler),
             _loader(val_ds, transforms_map["eval"], batch_size, num_workers),
             _loader(test_ds, transforms_map["eval"], batch_size, num_workers),
@@ -321,7 +327,7 @@ def evaluate_on_loader(model: nn.Module, data_loader: DataLoader, criterion: nn.
     y_true: List[torch.Tensor] = []
     y_pred: List[torch.Tensor] = []
     with torch.no_grad():
-        for batch in data_loader:
+        for batch in D.shard_loader(data_loader):
             inputs, labels = batch[:2]
             inputs = _to_device(inputs, device, model)
             labels = labels.to(device)
@@ -330,9 +336,11 @@ def evaluate_on_loader(model: nn.Module, data_loader: DataLoader, criterion: nn.
             losses.append(loss)
             y_true.append(labels)
             y_pred.append(pred)
-    avg = float(np.mean(torch.cat(losses).cpu().numpy().astype(np.float64))) if losses else 0.0
-    yt = torch.cat(y_true).cpu().numpy().tolist() if y_true else []
-    yp = torch.cat(y_pred).cpu().numpy().tolist() if y_pred else []
+    # per-batch losses / predictions in batch order (gathered in rank order under DP)
+    bl = D.gather_list(torch.cat(losses).cpu().numpy().astype(np.float64).tolist() if losses else [])
+    yt = D.gather_list(torch.cat(y_true).cpu().numpy().tolist() if y_true else [])
+    yp = D.gather_list(torch.cat(y_pred).cpu().numpy().tolist() if y_pred else [])
+    avg = float(np.mean(bl)) if bl else 0.0
     acc, f1 = compute_accuracy_f1(yt, yp)
     return avg, acc, f1
 
@@ -364,9 +372,11 @@ def train_model(model: nn.Module, train_loader: DataLoader, val_loader: DataLoad
             losses.append(loss.detach().view(1))
             yt.append(labels)
             yp.append(outputs.detach().argmax(dim=1))
-        tl = float(np.mean(torch.cat(losses).cpu().numpy().astype(np.float64))) if losses else 0.0
-        ta, tf1 = compute_accuracy_f1(torch.cat(yt).cpu().numpy().tolist() if yt else [],
-                                      torch.cat(yp).cpu().numpy().tolist() if yp else [])
+        # under DP the epoch's metrics cover every rank's steps (gathered in rank order)
+        sl = D.gather_list(torch.cat(losses).cpu().numpy().astype(np.float64).tolist() if losses else [])
+        tl = float(np.mean(sl)) if sl else 0.0
+        ta, tf1 = compute_accuracy_f1(D.gather_list(torch.cat(yt).cpu().numpy().tolist() if yt else []),
+                                      D.gather_list(torch.cat(yp).cpu().numpy().tolist() if yp else []))
         vl, va, vf1 = evaluate_on_loader(model, val_loader, criterion, device)
         if scheduler is not None:
             if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
@@ -382,7 +392,7 @@ def train_model(model: nn.Module, train_loader: DataLoader, val_loader: DataLoad
             best_val_loss = vl
             best_state = model.state_dict()
             patience = 0
-            if model_path is not None:
+            if model_path is not None and D.is_main():
                 model_path.parent.mkdir(parents=True, exist_ok=True)
                 torch.save(best_state, model_path)
         else:
@@ -398,7 +408,9 @@ def make_optimizer(model: SSIPResNet, lr: float, weight_decay: float, params=Non
     """optim.AdamW((p for p in model.parameters() if p.requires_grad), lr, wd) on the fused kernel."""
     arena = model.flatten_parameters()
     ps = [p for p in (params if params is not None else model.parameters()) if p.requires_grad]
-    return AdamW(ps, lr=lr, weight_decay=weight_decay, arena=arena)
+    opt = AdamW(ps, lr=lr, weight_decay=weight_decay, arena=arena)
+    D.attach_grad_allreduce(model, opt)  # no-op on one process
+    return opt
 
 
 # ---------------------------------------------------------------------------
@@ -414,7 +426,7 @@ def evaluate_model(model: nn.Module, data_loader: DataLoader, device: torch.devi
     y_prob: List[float] = []
     paths_all: List[str] = []
     with torch.no_grad():
-        for batch in data_loader:
+        for batch in D.shard_loader(data_loader):
             inputs, labels = batch[:2]
             extras = batch[2:] if len(batch) > 2 else []
             paths = extras[0] if extras else ["" for _ in range(len(labels))]
@@ -433,6 +445,8 @@ def evaluate_model(model: nn.Module, data_loader: DataLoader, device: torch.devi
             y_pred.extend(pred.tolist())
             y_prob.extend(probs.tolist())
             paths_all.extend(str(p) for p in list(paths))
+    if D.world() > 1:  # rank-ordered shards = the single-process order
+        y_true, y_pred, y_prob, paths_all = (D.gather_list(v) for v in (y_true, y_pred, y_prob, paths_all))
     if pos_index is not None:
         ytb = (np.array(y_true) == pos_index).astype(int)
         ypb = (np.array(y_pred) == pos_index).astype(int)
@@ -455,6 +469,8 @@ def _plt():
 
 
 def plot_training_curves(history: Dict[str, List[float]], output_path: Path, title: str) -> None:
+    if not D.is_main():
+        return
     plt = _plt()
     ep = range(1, len(history["train_loss"]) + 1)
     fig, ax = plt.subplots(1, 2, figsize=(10, 4))
@@ -473,6 +489,8 @@ def plot_training_curves(history: Dict[str, List[float]], output_path: Path, tit
 
 
 def plot_confusion_matrix(y_true, y_pred, class_names: Sequence[str], output_path: Path) -> None:
+    if not D.is_main():
+        return
     plt = _plt()
     mat = confusion_matrix(y_true, y_pred)
     fig = plt.figure(figsize=(4, 4))
@@ -495,6 +513,8 @@ def plot_confusion_matrix(y_true, y_pred, class_names: Sequence[str], output_pat
 
 
 def plot_roc_curves(curves: Dict[str, Tuple[np.ndarray, np.ndarray]], output_path: Path) -> None:
+    if not D.is_main():
+        return
     plt = _plt()
     fig = plt.figure(figsize=(6, 6))
     for label, (yt, yp) in curves.items():
@@ -512,6 +532,8 @@ def plot_roc_curves(curves: Dict[str, Tuple[np.ndarray, np.ndarray]], output_pat
 
 
 def plot_pr_curves(curves: Dict[str, Tuple[np.ndarray, np.ndarray]], output_path: Path) -> None:
+    if not D.is_main():
+        return
     plt = _plt()
     fig = plt.figure(figsize=(6, 6))
     for label, (yt, yp) in curves.items():
@@ -545,6 +567,8 @@ def compute_binary_confusion_metrics(y_true: np.ndarray, y_pred: np.ndarray, pos
 
 
 def plot_metrics_bars(metrics_map: Dict[str, Dict[str, float]], output_path: Path, keys: Sequence[str]) -> None:
+    if not D.is_main():
+        return
     plt = _plt()
     labels = list(metrics_map)
     x = np.arange(len(labels))

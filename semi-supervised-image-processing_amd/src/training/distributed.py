@@ -1,0 +1,128 @@
+"""Data parallelism for the drop-in pipelines (build extension: the reference
+is single-process).
+
+Launch any of the three CLIs under torchrun (one process per GPU, RCCL via
+torch.distributed "nccl"); without WORLD_SIZE > 1 everything here is the
+identity and the pipelines are exactly the single-process reference path.
+
+What is sharded, and how the result stays equal to the single-process one:
+  * evaluation / pseudo-labelling / triage / extraction (forward-only, eval-mode
+    BN: every image's output is independent of its batch): the loader's BATCHES
+    are split contiguously over the ranks (``shard_loader``), so every rank sees
+    the same batch compositions as the single process, and per-batch results
+    are gathered in rank order (``gather_list``) -- the reference's per-batch
+    loss mean, prediction order and pseudo-label list come out identical
+    (reference: semi_supervised.py:44-72, common.py:317-342,439-506,
+    feature_extraction.py:251-313);
+  * training: the balanced WeightedRandomSampler stream is drawn identically on
+    every rank (same global RNG) and rank-strided (``RankStridedSampler``); the
+    gradients are all-reduced in buckets during the backward (ssip.dist) and the
+    1/world average is folded into the fused AdamW (DDP semantics: per-rank
+    BatchNorm statistics, initial weights and buffers broadcast from rank 0);
+  * artifacts are written by rank 0 only (``is_main``).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Iterator, List, Optional
+
+import torch
+import torch.distributed as dist
+from torch.utils.data import DataLoader, Sampler, Subset
+
+from ssip.dist import GradBucketer, gather_objects, init_from_env, shard_range
+
+
+def setup(device: torch.device) -> torch.device:
+    """Initialise the process group when launched by torchrun (WORLD_SIZE > 1)
+    and return this rank's device (cuda:LOCAL_RANK)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        _, _, local = init_from_env()
+        if device.type == "cuda":
+            n = torch.cuda.device_count()
+            device = torch.device("cuda", local % n if n else 0)
+            torch.cuda.set_device(device)
+    return device
+
+
+def world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def is_main() -> bool:
+    return rank() == 0
+
+
+def shard_loader(loader: DataLoader) -> DataLoader:
+    """This rank's contiguous run of the loader's batches (same batch size,
+    collate and workers; sequential loaders only)."""
+    w = world()
+    if w == 1:
+        return loader
+    if loader.batch_size is None:
+        raise ValueError("shard_loader needs a batched loader")
+    ds = loader.dataset
+    n, bs = len(ds), loader.batch_size
+    nb = math.ceil(n / bs) if not loader.drop_last else n // bs
+    blo, bhi = shard_range(nb, rank(), w)
+    idx = list(range(blo * bs, min(bhi * bs, n)))
+    return DataLoader(Subset(ds, idx), batch_size=bs, shuffle=False, num_workers=loader.num_workers,
+                      pin_memory=loader.pin_memory, collate_fn=loader.collate_fn, drop_last=loader.drop_last)
+
+
+def gather_list(local: list) -> list:
+    """Per-rank lists concatenated in rank order (identity on one process)."""
+    return gather_objects(local) if world() > 1 else list(local)
+
+
+class RankStridedSampler(Sampler):
+    """The base sampler's stream, drawn identically on every rank (it consumes
+    the global torch RNG like the reference's WeightedRandomSampler does at each
+    epoch's iter), rank-strided: rank r trains on draws r, r + world, ..."""
+
+    def __init__(self, base: Sampler, rank_: Optional[int] = None, world_: Optional[int] = None):
+        self.base = base
+        self.r = rank() if rank_ is None else rank_
+        self.w = world() if world_ is None else world_
+
+    def __iter__(self) -> Iterator[int]:
+        return iter(list(self.base)[self.r::self.w])
+
+    def __len__(self) -> int:
+        n = len(self.base)
+        return (n - self.r + self.w - 1) // self.w if n > self.r else 0
+
+
+def broadcast_model(model) -> None:
+    """Rank 0's weights and BN buffers on every rank (DDP initial sync)."""
+    if world() == 1:
+        return
+    arena = model.flatten_parameters()
+    dist.broadcast(arena.flat, 0)
+    for b in model.buffers():
+        dist.broadcast(b, 0)
+
+
+def attach_grad_allreduce(model, optimizer) -> None:
+    """Bucketed gradient all-reduce launched from inside the backward; the
+    optimizer's step() waits for it and averages (grad_scale = 1/world)."""
+    if world() == 1:
+        return
+    broadcast_model(model)
+    bucketer = GradBucketer(model.flatten_parameters())
+    model.grad_ready_hook = bucketer.mark_ready
+    optimizer.dp_bucketer = bucketer
+
+
+def rank_sum(values: List[float]) -> List[float]:
+    """Element-wise sum over ranks (host floats)."""
+    if world() == 1:
+        return list(values)
+    t = torch.tensor(values, dtype=torch.float64)
+    dist.all_reduce(t)
+    return t.tolist()

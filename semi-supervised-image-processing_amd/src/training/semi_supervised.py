@@ -23,6 +23,7 @@ from torch.utils.data import DataLoader
 from ssip import ops
 from ssip.data import Collate
 
+from . import distributed as D
 from .common import (
     CrossEntropyLoss,
     PseudoLabeledDataset,
@@ -58,7 +59,7 @@ def generate_pseudo_labels(model: nn.Module, data_loader: DataLoader, device: to
     model.eval()
     out: List[Tuple[str, int, float]] = []
     with torch.no_grad():
-        for images, paths in data_loader:
+        for images, paths in D.shard_loader(data_loader):
             images = _to_device(images, device, model)
             logits = model(images)
             _, conf, pred, keep, _ = ops.softmax_select(logits, float(threshold), 0)
@@ -67,6 +68,7 @@ def generate_pseudo_labels(model: nn.Module, data_loader: DataLoader, device: to
             for path, p, cf in zip(paths, pr, c):
                 if cf >= np.float32(threshold):
                     out.append((path, int(p), float(cf)))
+    out = D.gather_list(out)  # rank-ordered shards of the pool = the single-process order
     LOGGER.info("Generated %d pseudo-labelled samples with threshold %.2f", len(out), threshold)
     return out
 
@@ -123,6 +125,89 @@ def _filter_cohort(ds: UnlabeledImageDataset, cfg: TrainingConfig) -> None:
         raise RuntimeError("Cohort filtering removed all unlabeled images; check the CSV paths match --weak-data-dir.")
 
 
+class _Raw:
+    """uint8 pixels of a dataset's images (decode only; the consistency step
+    draws and applies its own weak / strong views on the device)."""
+
+    def __init__(self, paths_labels):
+        self.items = list(paths_labels)
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        from ssip.data import pil_loader
+
+        path, label = self.items[i]
+        return torch.from_numpy(np.ascontiguousarray(np.asarray(pil_loader(path)))), label
+
+
+def _stack(batch):
+    imgs = [b[0] for b in batch]
+    if len({tuple(t.shape) for t in imgs}) != 1:
+        raise ValueError("--consistency needs equally sized images within a batch")
+    return torch.stack(imgs), torch.tensor([b[1] for b in batch], dtype=torch.int64)
+
+
+def train_consistency(model, base, train_idx, pool, val_loader, criterion, device, config: TrainingConfig):
+    """Joint weak/strong consistency training (ssip.semi_step.SemiStep, the
+    benchmarked step) for config.weak_pretrain_epochs epochs: each step pairs
+    a balanced-sampled labelled batch with the next unlabelled batch of the
+    pool; tau = --pseudo-threshold (reference rule, semi_supervised.py:60-66),
+    loss = CE(labelled) + lambda_u * mean_u[mask * CE(strong, pseudo)].  The
+    history has the reference's six keys (train_* over the labelled part)."""
+    from ssip.dist import GradBucketer
+    from ssip.semi_step import SemiStep
+
+    from .common import compute_accuracy_f1, evaluate_on_loader
+
+    D.broadcast_model(model)  # rank 0's initial weights and buffers on every rank
+    bucketer = GradBucketer(model.flatten_parameters()) if D.world() > 1 else None
+    step = SemiStep(model, lr=config.learning_rate, weight_decay=config.weight_decay,
+                    tau=config.pseudo_label_threshold, lambda_u=config.lambda_u, image_size=config.image_size,
+                    bucketer=bucketer, seed=config.seed + D.rank())
+    bs = config.batch_size
+    lab = _Raw([base.samples[int(i)] for i in train_idx])
+    sampler = make_balanced_sampler([base.samples[int(i)][1] for i in train_idx])
+    if D.world() > 1:
+        sampler = D.RankStridedSampler(sampler)
+    lab_loader = DataLoader(lab, batch_size=bs, sampler=sampler, num_workers=config.num_workers, collate_fn=_stack,
+                            drop_last=True)
+    unl = _Raw([(str(p), -1) for p in pool.image_paths])
+    gen = torch.Generator().manual_seed(config.seed)
+    history: Dict[str, List[float]] = {k: [] for k in
+                                       ("train_loss", "val_loss", "train_acc", "val_acc", "train_f1", "val_f1")}
+    for epoch in range(config.weak_pretrain_epochs):
+        model.train()
+        order = torch.randperm(len(unl), generator=gen).tolist()
+        unl_loader = D.shard_loader(DataLoader(torch.utils.data.Subset(unl, order), batch_size=bs, shuffle=False,
+                                               num_workers=config.num_workers, collate_fn=_stack, drop_last=True))
+        lab_iter = iter(lab_loader)
+        losses, yt, yp = [], [], []
+        for xu, _ in unl_loader:
+            try:
+                xl, yl = next(lab_iter)
+            except StopIteration:
+                lab_iter = iter(lab_loader)
+                xl, yl = next(lab_iter)
+            out = step(xl.to(device, non_blocking=True), yl.to(device), xu.to(device, non_blocking=True))
+            losses.append(out.loss[0:1].clone())
+            yt.append(yl)
+            yp.append(step.last["logits"][: yl.shape[0]].argmax(1).cpu())
+        sl = D.gather_list(torch.cat(losses).cpu().double().tolist() if losses else [])
+        tl = float(np.mean(sl)) if sl else 0.0
+        ta, tf1 = compute_accuracy_f1(D.gather_list(torch.cat(yt).tolist() if yt else []),
+                                      D.gather_list(torch.cat(yp).tolist() if yp else []))
+        vl, va, vf1 = evaluate_on_loader(model, val_loader, criterion, device)
+        for k, v in zip(("train_loss", "val_loss", "train_acc", "val_acc", "train_f1", "val_f1"),
+                        (tl, vl, ta, va, tf1, vf1)):
+            history[k].append(v)
+        LOGGER.info("Consistency epoch %d/%d - train loss %.4f acc %.3f | val loss %.4f acc %.3f f1 %.3f",
+                    epoch + 1, config.weak_pretrain_epochs, tl, ta, vl, va, vf1)
+    model.grad_ready_hook = None
+    return history
+
+
 def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
     set_seed(config.seed)
     device = resolve_device(config.device)
@@ -163,23 +248,29 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
     pseudo_ds = PseudoLabeledDataset([(p, l) for p, l, _ in pseudo], transform=tfm["train"])
     if len(pseudo_ds) == 0:
         raise RuntimeError("No pseudo-labelled samples were generated. Try lowering the threshold.")
-    pseudo_loader = DataLoader(pseudo_ds, batch_size=config.batch_size,
-                               sampler=make_balanced_sampler([l for _, l, _ in pseudo]),
+    pseudo_sampler = make_balanced_sampler([l for _, l, _ in pseudo])
+    if D.world() > 1:
+        pseudo_sampler = D.RankStridedSampler(pseudo_sampler)
+    pseudo_loader = DataLoader(pseudo_ds, batch_size=config.batch_size, sampler=pseudo_sampler,
                                num_workers=config.num_workers, pin_memory=torch.cuda.is_available(),
                                collate_fn=Collate(tfm["train"]))
 
     # frozen-backbone pretrain (BN still in train mode), then fine-tune
     semi = create_model(num_classes, pretrained=True, dtype=config.dtype, weights=config.weights,
                            allow_random_init=config.random_init).to(device)
-    for name, p in semi.named_parameters():
-        if not name.startswith("fc"):
-            p.requires_grad = False
-    opt_p = make_optimizer(semi, config.learning_rate, config.weight_decay)
-    sch_p = torch.optim.lr_scheduler.ReduceLROnPlateau(opt_p, mode="min", patience=2, factor=0.5)
     t0 = time.time()
-    semi, pre_hist = train_model(semi, pseudo_loader, val_loader, criterion, opt_p, device, scheduler=sch_p,
-                                 num_epochs=config.weak_pretrain_epochs,
-                                 early_stopping_patience=config.early_stopping_patience)
+    if config.consistency:
+        # build extension (BASELINE config 3): joint consistency training in place of the pretrain
+        pre_hist = train_consistency(semi, base, splits["train"], pool, val_loader, criterion, device, config)
+    else:
+        for name, p in semi.named_parameters():
+            if not name.startswith("fc"):
+                p.requires_grad = False
+        opt_p = make_optimizer(semi, config.learning_rate, config.weight_decay)
+        sch_p = torch.optim.lr_scheduler.ReduceLROnPlateau(opt_p, mode="min", patience=2, factor=0.5)
+        semi, pre_hist = train_model(semi, pseudo_loader, val_loader, criterion, opt_p, device, scheduler=sch_p,
+                                     num_epochs=config.weak_pretrain_epochs,
+                                     early_stopping_patience=config.early_stopping_patience)
     for p in semi.parameters():
         p.requires_grad = True
     opt_f = make_optimizer(semi, config.learning_rate / 2, config.weight_decay)
@@ -196,9 +287,10 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
     # artifacts (reference :360-511)
     payload = {"baseline": base_hist, "semi_pretrain": pre_hist, "semi_finetune": fin_hist,
                "splits": {k: v.tolist() for k, v in splits.items()}, "pseudo_label_count": len(pseudo)}
-    config.history_path.parent.mkdir(parents=True, exist_ok=True)
-    with open(config.history_path, "w", encoding="utf-8") as fp:
-        json.dump(payload, fp, indent=2)
+    if D.is_main():
+        config.history_path.parent.mkdir(parents=True, exist_ok=True)
+        with open(config.history_path, "w", encoding="utf-8") as fp:
+            json.dump(payload, fp, indent=2)
     joined = {k: pre_hist[k] + fin_hist[k] for k in pre_hist}
     plot_training_curves(joined, config.semi_curve_path, "Semi-supervised")
     plot_confusion_matrix(b_true, b_pred, base.classes, config.baseline_confusion_path)
@@ -225,22 +317,24 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
         "target_recall": None if config.target_recall is None else float(config.target_recall),
         "training_time_sec": s_thr.get("training_time_sec", semi_time),
         "min_precision": s_thr.get("min_precision"), "max_fpr": s_thr.get("max_fpr")}
-    Path("outputs/tables").mkdir(parents=True, exist_ok=True)
-    pd.DataFrame.from_dict(rows, orient="index").to_csv(Path("outputs/tables/results_comparison_detailed.csv"))
+    if D.is_main():
+        Path("outputs/tables").mkdir(parents=True, exist_ok=True)
+        pd.DataFrame.from_dict(rows, orient="index").to_csv(Path("outputs/tables/results_comparison_detailed.csv"))
+        config.results_table.parent.mkdir(parents=True, exist_ok=True)
+        pd.DataFrame.from_dict({"baseline_thresholded": b_thr, "semi_thresholded": s_thr},
+                               orient="index").to_csv(config.results_table)
     plot_metrics_bars(rows, Path("outputs/figures/metrics_comparison.png"),
                       keys=["TPR", "FPR", "TNR", "precision", "accuracy"])
-    config.results_table.parent.mkdir(parents=True, exist_ok=True)
-    pd.DataFrame.from_dict({"baseline_thresholded": b_thr, "semi_thresholded": s_thr},
-                           orient="index").to_csv(config.results_table)
 
     try:
         op = {"model": "semi_supervised_resnet18", "checkpoint": str(config.semi_checkpoint),
               "positive_class": config.positive_class, "threshold": s_thr.get("threshold"),
               "policy": s_thr.get("threshold_policy"), "target_recall": config.target_recall,
               "min_precision": config.min_precision, "max_fpr": config.max_fpr, "seed": config.seed}
-        config.operating_point_path.parent.mkdir(parents=True, exist_ok=True)
-        with open(config.operating_point_path, "w", encoding="utf-8") as fp:
-            json.dump(op, fp, indent=2)
+        if D.is_main():
+            config.operating_point_path.parent.mkdir(parents=True, exist_ok=True)
+            with open(config.operating_point_path, "w", encoding="utf-8") as fp:
+                json.dump(op, fp, indent=2)
     except Exception as exc:  # reference: warn and continue
         LOGGER.warning("Failed to write operating_point.json: %s", exc)
 
@@ -253,14 +347,15 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
             semi.eval()
             recs = []
             with torch.no_grad():
-                for images, paths in tri_loader:
+                for images, paths in D.shard_loader(tri_loader):
                     logits = semi(_to_device(images, device, semi))
                     _, _, _, _, pos = ops.softmax_select(logits, 0.0, pos_index)
                     for pth, pr in zip(paths, pos.cpu().numpy().tolist()):
                         recs.append({"path": str(pth), "prob_positive": float(pr), "flagged": bool(pr >= float(tthr))})
-            df = pd.DataFrame(recs)
-            config.triage_csv_path.parent.mkdir(parents=True, exist_ok=True)
-            df.to_csv(config.triage_csv_path, index=False)
+            df = pd.DataFrame(D.gather_list(recs))
+            if D.is_main():
+                config.triage_csv_path.parent.mkdir(parents=True, exist_ok=True)
+                df.to_csv(config.triage_csv_path, index=False)
             LOGGER.info("Wrote triage CSV with %d rows (%d flagged) to %s", len(df),
                         int(df["flagged"].sum()) if not df.empty else 0, config.triage_csv_path)
         else:

@@ -9,6 +9,7 @@ from typing import Dict
 import pandas as pd
 import torch
 
+from . import distributed as D
 from .common import (
     CrossEntropyLoss,
     TrainingConfig,
@@ -73,6 +74,7 @@ def run_supervised(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
     yb = (t_true == pos_index).astype(int)
     plot_roc_curves({"Baseline": (yb, t_prob)}, config.roc_curve_path)
     plot_pr_curves({"Baseline": (yb, t_prob)}, Path("outputs/figures/pr_curves_baseline.png"))
-    config.results_table.parent.mkdir(parents=True, exist_ok=True)
-    pd.DataFrame.from_dict({"baseline_thresholded": thr_metrics}, orient="index").to_csv(config.results_table)
+    if D.is_main():
+        config.results_table.parent.mkdir(parents=True, exist_ok=True)
+        pd.DataFrame.from_dict({"baseline_thresholded": thr_metrics}, orient="index").to_csv(config.results_table)
     return {"baseline_thresholded": thr_metrics, "baseline_argmax": arg_metrics}

@@ -29,6 +29,14 @@ class AdamW(torch.optim.Optimizer):
         self._runs_cache: Dict[int, List[Tuple[int, int, List[torch.Tensor]]]] = {}
         self._sched = None     # per group: fp64 device tensor {lr, t, lr/(1-b1^t), sqrt(1-b2^t)}
         self._sched_lr = None
+        # data parallelism (src/training/distributed.attach_grad_allreduce): a
+        # GradBucketer whose all-reduces step() waits for, averaging by 1/world
+        self.dp_bucketer = None
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        super().zero_grad(set_to_none=set_to_none)
+        if self.dp_bucketer is not None:
+            self.dp_bucketer.reset()
 
     def use_device_schedule(self) -> None:
         """Keep lr and the step count on the device (``ssip_adamw_sched_step``
@@ -82,6 +90,8 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self.dp_bucketer is not None:
+            grad_scale = grad_scale * self.dp_bucketer.finish()
         self._ensure_flat_state()
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]

@@ -89,3 +89,58 @@ def test_shard_range_covers_everything():
             spans = [shard_range(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def _pipeline_worker(rank, world, port, q):
+    """The drop-in pipelines' DP helpers (src/training/distributed.py)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        from pathlib import Path
+
+        from torch.utils.data import DataLoader, WeightedRandomSampler
+
+        root = Path(__file__).resolve().parents[1]
+        sys.path.insert(0, str(root / "semi-supervised-image-processing_amd"))
+        from src.training import distributed as D
+
+        ok = D.world() == world and D.rank() == rank and D.is_main() == (rank == 0)
+        # batch-granular sharding: every rank sees whole batches of the
+        # single-process loader, and the rank-ordered gather restores its order
+        data = [(float(i), i % 3) for i in range(11)]
+        full = DataLoader(data, batch_size=3, shuffle=False)
+        single = [b[0].tolist() for b in full]
+        mine = [b[0].tolist() for b in D.shard_loader(full)]
+        ok &= D.gather_list(mine) == single
+        # per-batch means (the reference's evaluate_on_loader loss) are unchanged
+        ok &= D.gather_list([sum(b) / len(b) for b in mine]) == [sum(b) / len(b) for b in single]
+        # the balanced sampler's stream is drawn identically on every rank and strided
+        torch.manual_seed(5)
+        w = [1.0, 3.0, 1.0, 1.0, 2.0, 1.0, 1.0]
+        glob = list(WeightedRandomSampler(w, num_samples=7, replacement=True))
+        torch.manual_seed(5)
+        s = D.RankStridedSampler(WeightedRandomSampler(w, num_samples=7, replacement=True))
+        local = list(s)
+        ok &= local == glob[rank::world] and len(s) == len(local)
+        parts = D.gather_list([local])
+        inter = [x for t in zip(*[p + [None] * (len(parts[0]) - len(p)) for p in parts]) for x in t if x is not None]
+        ok &= inter == glob
+        ok &= D.rank_sum([1.0, float(rank)]) == [float(world), float(sum(range(world)))]
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipeline_sharding_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: True, 1: True}
+    assert all(p.exitcode == 0 for p in procs)

@@ -1,0 +1,176 @@
+"""GPU, data parallel with 2 ranks sharing one MI355X (gloo carries the
+collectives; RCCL's "nccl" backend takes its place on a multi-GPU node with
+the same code): the benchmarked SemiStep with the bucketed gradient
+all-reduce launched from inside the real backward (hook order, wgrad side
+stream hand-off), eager and launch-plan execution.
+
+Asserted:
+  * after one step the all-reduced gradient arena equals the SUM of the two
+    single-process gradients of the ranks' shards (the 1/world average is
+    folded into AdamW), to fp32 rounding of one add;
+  * after 4 steps both ranks hold identical weights (bitwise), and the
+    launch-plan replays equal the eager steps (bitwise).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+S, BL, BU, STEPS = 64, 64, 64, 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rank):
+    from ssip.augment import draw_params_batch
+
+    g = torch.Generator().manual_seed(100 + rank)
+    x_l = torch.randint(0, 256, (BL, S, S, 3), generator=g, dtype=torch.uint8)
+    x_u = torch.randint(0, 256, (BU, S, S, 3), generator=g, dtype=torch.uint8)
+    y_l = torch.randint(0, 2, (BL,), generator=g)
+    params = [(draw_params_batch(BL, S, False, g), draw_params_batch(BU, S, False, g), draw_params_batch(BU, S, True, g))
+              for _ in range(STEPS)]
+    return x_l, y_l, x_u, params
+
+
+def _make(dev, bucketer_world=False, plan=False):
+    from ssip import SSIPResNet, replace_fc
+    from ssip.dist import GradBucketer
+    from ssip.semi_step import SemiStep
+
+    torch.manual_seed(0)
+    m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2).to(dev).train()
+    bucketer = GradBucketer(m.flatten_parameters(), bucket_bytes=8 << 20) if bucketer_world else None
+    step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=S, bucketer=bucketer, seed=0, plan=plan)
+    step.opt.use_device_schedule()
+    return step
+
+
+def _worker(rank, world, port, plan, out):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "semi-supervised-image-processing_amd"), str(root)]
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        step = _make(dev, bucketer_world=True, plan=plan)
+        x_l, y_l, x_u, params = _data(rank)
+        x_l, y_l, x_u = x_l.to(dev), y_l.to(dev), x_u.to(dev)
+        res = {}
+        for i in range(STEPS):
+            step(x_l, y_l, x_u, params[i])
+            if i == 0:
+                torch.cuda.synchronize()
+                res["grad0"] = step.arena.grad.detach().cpu().clone()
+        torch.cuda.synchronize()
+        res["flat"] = step.arena.flat.detach().cpu().clone()
+        res["plan_ops"] = step._plan.num_ops if plan else 0
+        torch.save(res, os.path.join(out, f"rank{rank}_{'plan' if plan else 'eager'}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, plan, out):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, plan, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(200)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_semi_step_dp2_gloo(dev, tmp_path):
+    _run(2, False, str(tmp_path))
+    _run(2, True, str(tmp_path))
+    r = {(k, m): torch.load(tmp_path / f"rank{k}_{m}.pt", weights_only=True) for k in (0, 1) for m in ("eager", "plan")}
+    # identical weights on both ranks, eager and plan alike, and plan == eager
+    for m in ("eager", "plan"):
+        assert torch.equal(r[(0, m)]["flat"], r[(1, m)]["flat"]), m
+    assert torch.equal(r[(0, "eager")]["flat"], r[(0, "plan")]["flat"])
+    assert r[(0, "plan")]["plan_ops"] > 100
+    # the reduced gradient = sum of the per-rank single-process gradients
+    singles = []
+    for rank in (0, 1):
+        step = _make(dev)
+        x_l, y_l, x_u, params = _data(rank)
+        step(x_l.to(dev), y_l.to(dev), x_u.to(dev), params[0])
+        torch.cuda.synchronize()
+        singles.append(step.arena.grad.detach().cpu().clone())
+    want = singles[0] + singles[1]
+    for m in ("eager", "plan"):
+        got = r[(0, m)]["grad0"]
+        err = ((got - want).abs().max() / want.abs().max()).item()
+        assert err <= 1e-6, (m, err)
+        assert torch.equal(got, r[(1, m)]["grad0"])
+
+
+def _fe_worker(rank, world, port, data, cwd):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "semi-supervised-image-processing_amd"), str(root)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), SSIP_DIST_BACKEND="gloo")
+    os.chdir(cwd)
+    import torch.distributed as dist
+
+    from src import feature_extraction as FE
+
+    try:
+        FE.main(["--data-dir", data, "--batch-size", "5", "--random-init"])
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_feature_extraction_dp2_equals_single(dev, tmp_path, monkeypatch):
+    """`python -m src.feature_extraction` under 2 ranks (file list sharded by
+    whole batches, embeddings gathered in rank order) writes the same
+    embeddings.npy / embeddings.csv as the single-process run, bit for bit."""
+    import numpy as np
+
+    from test_gpu_pipeline import _make_dataset
+
+    data = _make_dataset(tmp_path / "mri", n_per_class=7, n_unl=9, size=80)
+    (tmp_path / "dp").mkdir()
+    (tmp_path / "single").mkdir()
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_fe_worker, args=(r, 2, port, str(data), str(tmp_path / "dp"))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(200)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    monkeypatch.chdir(tmp_path / "single")
+    from src import feature_extraction as FE
+
+    FE.main(["--data-dir", str(data), "--batch-size", "5", "--random-init"])
+    a = np.load(tmp_path / "dp/outputs/features/embeddings.npy")
+    b = np.load(tmp_path / "single/outputs/features/embeddings.npy")
+    assert a.shape == b.shape == (23, 512)
+    assert np.array_equal(a, b)
+    assert (tmp_path / "dp/outputs/features/embeddings.csv").read_text() == \
+        (tmp_path / "single/outputs/features/embeddings.csv").read_text()

@@ -153,6 +153,13 @@ def test_cli_end_to_end(dev, tmp_path, monkeypatch):
         assert (tmp_path / "outputs" / f).exists(), f
     sd = torch.load(tmp_path / "outputs/models/semi_resnet18.pt", weights_only=True)
     assert len(sd) == 122 and "layer4.1.bn2.running_var" in sd
+    # config 3 through the drop-in CLI: joint consistency training in the semi stage
+    S.main(common + ["--weak-data-dir", str(data / "sans_label"), "--baseline-epochs", "1",
+                     "--weak-pretrain-epochs", "2", "--finetune-epochs", "1", "--pseudo-threshold", "0.5",
+                     "--consistency", "--dtype", "bf16"])
+    hist = json.loads((tmp_path / "outputs/notes/training_history.json").read_text())
+    assert len(hist["semi_pretrain"]["train_loss"]) == 2
+    assert all(np.isfinite(v) for v in hist["semi_pretrain"]["train_loss"])
     FE.main(["--data-dir", str(data), "--batch-size", "8", "--random-init"])
     emb = np.load(tmp_path / "outputs/features/embeddings.npy")
     assert emb.shape == (36, 512) and emb.dtype == np.float32

@@ -187,9 +187,150 @@ def main() -> None:
     recs_ref = FE.discover_image_records(data)
     goldens["extraction"]["records"] = [[str(r.relative_path), r.bucket, r.label] for r in recs_ref]
 
+    # 8b. the schema of the reference's COMMITTED extraction artifacts
+    #     (outputs/features/metadata.json, outputs/notes/feature_summary.md)
+    meta = json.loads((REF / "outputs/features/metadata.json").read_text())
+    summary = (REF / "outputs/notes/feature_summary.md").read_text().splitlines()
+    goldens["committed_metadata"] = {
+        "keys": list(meta), "sanity_keys": list(meta["sanity_checks"]),
+        "probe_keys": list(meta["neighbor_probe"][0]), "embedding_dimension": meta["embedding_dimension"],
+        "summary_headings": [ln for ln in summary if ln.startswith("#")],
+        "summary_bullets": [ln.split(":")[0] for ln in summary if ln.startswith("- ") and ":" in ln]}
+
+    # 9. the reference's own run_pipeline and run_supervised, end to end on a
+    #    tiny deterministic dataset (tests/golden/tiny_dataset.py) with a seeded
+    #    stand-in for the ImageNet weights: history, splits, pseudo-labels,
+    #    every table / JSON artifact (columns and values)
+    goldens["pipeline"] = _pipelines(C, SS)
+
+    # 10. the DataLoader worker stream: (flip, angle) each sample of the train
+    #     loader draws inside its worker (num_workers=2), 2 epochs
+    goldens["worker_stream"] = _worker_stream(C)
+
     with open(OUT / "goldens.json", "w") as f:
         json.dump(goldens, f, indent=1, default=float)
     print("wrote", sorted(p.name for p in OUT.iterdir()))
+
+
+PIPE_CFG = dict(batch_size=4, image_size=64, num_workers=0, baseline_epochs=2, weak_pretrain_epochs=1,
+                finetune_epochs=1, pseudo_label_threshold=0.5, target_recall=0.9, min_precision=0.5, seed=42)
+
+
+def _read_artifacts(out: Path, semi: bool) -> dict:
+    import pandas as pd
+
+    def table(p):
+        df = pd.read_csv(p, index_col=0)
+        if "training_time_sec" in df.columns:  # wall time: not reproducible, kept out of the fixture
+            df["training_time_sec"] = None
+        return {"columns": list(df.columns), "index": [str(i) for i in df.index],
+                "values": json.loads(df.to_json(orient="split"))["data"]}
+
+    art = {"results_comparison": table(out / "tables/results_comparison.csv")}
+    if semi:
+        art["history"] = json.loads((out / "notes/training_history.json").read_text())
+        art["results_comparison_detailed"] = table(out / "tables/results_comparison_detailed.csv")
+        art["operating_point"] = json.loads((out / "notes/operating_point.json").read_text())
+        tri = pd.read_csv(out / "tables/unlabeled_predictions_semi.csv")
+        art["triage"] = {"columns": list(tri.columns), "path": [Path(p).name for p in tri["path"]],
+                         "prob_positive": tri["prob_positive"].tolist(), "flagged": tri["flagged"].tolist()}
+    art["files"] = sorted(str(p.relative_to(out)) for p in out.rglob("*") if p.is_file())
+    return art
+
+
+def _pipelines(C, SS) -> dict:
+    import os
+
+    import torch
+
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(OUT))
+    import tiny_dataset
+    from training import supervised as SV  # reference module
+
+    res = {"config": PIPE_CFG, "weights_seed": 1234}
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        data = tiny_dataset.make(td / "mri")
+        wpath = td / "w.pt"
+        torch.save(tiny_dataset.pretrained_state_dict(1234), wpath)
+        os.environ["SSIP_RESNET18_WEIGHTS"] = str(wpath)
+        picks = []
+        real = SS.generate_pseudo_labels
+
+        def spy(*a, **k):
+            out = real(*a, **k)
+            picks.extend([Path(p).name, int(l), float(c)] for p, l, c in out)
+            return out
+
+        try:
+            for kind in ("semi", "supervised"):
+                (td / kind).mkdir()
+                os.chdir(td / kind)
+                cfg = C.TrainingConfig(strong_data_dir=data / "avec_labels", weak_data_dir=data / "sans_label",
+                                       device="cpu", **PIPE_CFG)
+                if kind == "semi":
+                    SS.generate_pseudo_labels = spy
+                    metrics = SS.run_pipeline(cfg)
+                    SS.generate_pseudo_labels = real
+                else:
+                    cfg.weak_pretrain_epochs, cfg.finetune_epochs, cfg.pseudo_label_threshold = 0, 0, 0.0
+                    metrics = SV.run_supervised(cfg)
+                for m in metrics.values():
+                    if "training_time_sec" in m:
+                        m["training_time_sec"] = None
+                res[kind] = {"metrics": json.loads(json.dumps(metrics, default=float)),
+                             "artifacts": _read_artifacts(td / kind / "outputs", kind == "semi")}
+            res["semi"]["pseudo_labels"] = picks
+        finally:
+            os.chdir(cwd)
+            os.environ.pop("SSIP_RESNET18_WEIGHTS", None)
+            SS.generate_pseudo_labels = real
+    return res
+
+
+class _Recorder:
+    """Wraps the reference's train Compose: replays the draws its
+    RandomHorizontalFlip / RandomRotation will make (same RNG state, restored)
+    and returns them beside the transformed image."""
+
+    def __init__(self, tf):
+        self.tf = tf
+
+    def __call__(self, img):
+        import torch
+
+        st = torch.get_rng_state()
+        flip = bool(torch.rand(1) < 0.5)
+        angle = float(torch.empty(1).uniform_(-10.0, 10.0).item())
+        torch.set_rng_state(st)
+        return self.tf(img), flip, angle
+
+
+def _worker_stream(C) -> dict:
+    import torch
+
+    sys.path.insert(0, str(OUT))
+    import tiny_dataset
+
+    with tempfile.TemporaryDirectory() as td:
+        data = tiny_dataset.make(Path(td) / "mri", n_per_class=8, n_unl=0, size=40)
+        C.set_seed(42)
+        tfs = C.build_transforms(32)
+        tfs = {"train": _Recorder(tfs["train"]), "eval": tfs["eval"]}
+        train_loader, _, _, base, splits = C.prepare_dataloaders(data / "avec_labels", tfs, 3, 0.2, 0.2, 42,
+                                                                 num_workers=2)
+        epochs = []
+        for _ in range(2):
+            ep = {"labels": [], "flip": [], "angle": []}
+            for (img, flips, angles), labels in train_loader:
+                ep["labels"] += labels.tolist()
+                ep["flip"] += [bool(f) for f in flips]
+                ep["angle"] += [float(a) for a in angles]
+            epochs.append(ep)
+    return {"n_per_class": 8, "size": 40, "image_size": 32, "batch_size": 3, "num_workers": 2, "seed": 42,
+            "train_idx": splits["train"].tolist(), "epochs": epochs}
 
 
 if __name__ == "__main__":

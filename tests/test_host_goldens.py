@@ -149,3 +149,68 @@ def test_cli_random_init_flag():
     assert S.parse_args(["--strong-data-dir", "a", "--weak-data-dir", "b"]).random_init is False
     assert S.parse_args(["--strong-data-dir", "a", "--weak-data-dir", "b", "--random-init"]).random_init is True
     assert FE.parse_args(["--random-init"]).random_init is True
+
+
+def test_dataloader_worker_stream_matches_reference(tmp_path):
+    """The (flip, angle) each train sample draws inside its DataLoader worker
+    (num_workers=2, 2 epochs: worker w seeded base_seed + w, base_seed and the
+    balanced sampler's multinomial from the global RNG each epoch) equals the
+    reference's own loader's draws (tests/golden: the reference's
+    prepare_dataloaders with a recording wrapper around its train Compose)."""
+    import sys
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+    import tiny_dataset
+    from src.training import common as C
+    from ssip.augment import rotate_fixed_point
+
+    ws = GOLD["worker_stream"]
+    data = tiny_dataset.make(tmp_path / "mri", n_per_class=ws["n_per_class"], n_unl=0, size=ws["size"])
+    C.set_seed(ws["seed"])
+    tfs = C.build_transforms(ws["image_size"])
+    train_loader, _, _, _, splits = C.prepare_dataloaders(data / "avec_labels", tfs, ws["batch_size"], 0.2, 0.2,
+                                                          ws["seed"], num_workers=ws["num_workers"])
+    assert splits["train"].tolist() == ws["train_idx"]
+    S = ws["image_size"]
+    for ep in ws["epochs"]:
+        labels, params = [], []
+        for batch, lab in train_loader:
+            labels += lab.tolist()
+            params.append(batch.params)
+        p = torch.cat(params)
+        assert labels == ep["labels"]
+        assert [bool(f) for f in p[:, 0]] == ep["flip"]
+        for row, ang in zip(p.tolist(), ep["angle"]):
+            assert tuple(row[2:8]) == rotate_fixed_point(ang, S, S)
+
+
+def test_extraction_artifact_schema_matches_committed(tmp_path, monkeypatch):
+    """metadata.json (keys and their order, sanity / neighbour-probe sub-keys)
+    and feature_summary.md (headings, bullet labels) as the reference's
+    committed outputs/features/metadata.json and outputs/notes/feature_summary.md
+    have them (feature_extraction.py:401-502)."""
+    import json as _json
+
+    from src import feature_extraction as FE
+
+    monkeypatch.chdir(tmp_path)
+    cm = GOLD["committed_metadata"]
+    e = np.random.default_rng(1).normal(size=(6, 512)).astype(np.float32)
+    img = tmp_path / "mri" / "sans_label"
+    img.mkdir(parents=True)
+    recs = []
+    for i in range(6):
+        f = img / f"{i}.jpg"
+        f.write_bytes(b"x")
+        recs.append(FE.ImageRecord(f, Path(f"sans_label/{i}.jpg"), "unlabeled", None))
+    res = FE.ExtractionResults(e, recs, [], [0.01] * 6, "random_init(seed=42)")
+    FE.save_artifacts(res, FE.run_sanity_checks(e), FE.nearest_neighbor_probe(e, recs), tmp_path / "mri", "cuda")
+    meta = _json.loads((tmp_path / "outputs/features/metadata.json").read_text())
+    assert list(meta) == cm["keys"]
+    assert list(meta["sanity_checks"]) == cm["sanity_keys"]
+    assert list(meta["neighbor_probe"][0]) == cm["probe_keys"]
+    assert meta["embedding_dimension"] == cm["embedding_dimension"]
+    md = (tmp_path / "outputs/notes/feature_summary.md").read_text().splitlines()
+    assert [ln for ln in md if ln.startswith("#")] == cm["summary_headings"]
+    assert [ln.split(":")[0] for ln in md if ln.startswith("- ") and ":" in ln] == cm["summary_bullets"]
+    assert np.load(tmp_path / "outputs/features/embeddings.npy").dtype == np.float32

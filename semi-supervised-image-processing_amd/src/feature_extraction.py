@@ -193,17 +193,27 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
         nb = (len(records) + batch_size - 1) // batch_size
         blo, bhi = shard_range(nb, D.rank(), D.world())
         mine = records[blo * batch_size:min(bhi * batch_size, len(records))]
+    chunks = list(batched(mine, batch_size))
     with ThreadPoolExecutor(max_workers=decode_threads) as pool:
-        for chunk in batched(mine, batch_size):
-            t0 = time.perf_counter()
+        # decode runs PREFETCH batches ahead of the device (Pillow releases the
+        # GIL while decoding); embeddings stay on the device until the end, so
+        # the loop never waits for the GPU
+        PREFETCH = 2
+        pending = [[pool.submit(decode, r) for r in c] for c in chunks[:PREFETCH]]
+        t_prev = time.perf_counter()
+        for ci in range(len(chunks)):
+            if ci + PREFETCH < len(chunks):
+                pending.append([pool.submit(decode, r) for r in chunks[ci + PREFETCH]])
             ok_recs, arrays = [], []
-            for rec, arr, exc in pool.map(decode, chunk):
+            for fut in pending[ci]:
+                rec, arr, exc = fut.result()
                 if exc is not None:
                     logging.error("Failed to decode %s: %s", rec.absolute_path, exc)
                     failures.append(rec.absolute_path)
                     continue
                 ok_recs.append(rec)
                 arrays.append(arr)
+            pending[ci] = None
             if not arrays:
                 continue
             with torch.no_grad():
@@ -212,10 +222,12 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
                     feats = model(tf(u8)).flatten(1)
                 else:
                     feats = torch.cat([model(tf(torch.from_numpy(a)[None].to(device))).flatten(1) for a in arrays])
-            embeddings.append(feats.cpu().numpy())
+            embeddings.append(feats)
             kept.extend(ok_recs)
-            per = (time.perf_counter() - t0) / len(ok_recs)
-            times.extend([per] * len(ok_recs))
+            t_now = time.perf_counter()
+            times.extend([(t_now - t_prev) / len(ok_recs)] * len(ok_recs))
+            t_prev = t_now
+    embeddings = [torch.cat(embeddings).cpu().numpy()] if embeddings else []
     if D.world() > 1:
         embeddings, kept, failures, times = (D.gather_list(v) for v in (embeddings, kept, failures, times))
     if not embeddings:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 4
+#define SSIP_ABI_VERSION 5
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -80,6 +80,14 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
 /* dx = conv_transpose(dy, w) (+ dx_add, nullable); w_crsk: [C][R][S][K] */
 int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, void* dx,
                     const void* dx_add, void* stream);
+/* dx = conv_transpose(dy, w) + conv_transpose_1x1/stride(dy_ds, w_ds): the
+ * input gradient of a downsampling BasicBlock (conv1 3x3/2 and the 1x1/2
+ * downsample share the block input; torchvision BasicBlock.forward).  wds_ck:
+ * [C][K] (the downsample's CRSK copy).  The bf16 stride-2 3x3 case runs as ONE
+ * phase-split launch (the downsample adds k-steps to the (even, even) phase);
+ * anything else runs the two dgrads back to back. */
+int ssip_conv_dgrad_ds(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dy_ds,
+                       const void* wds_ck, void* dx, void* stream);
 /* DGRAD with the next-lower BatchNorm's backward reduction fused into the
  * epilogue (replaces ssip_conv_dgrad + the reduce pass of ssip_bn_bwd):
  *   dpre = (dgrad(dy) + dx_add) * (zmask > 0)          [N][H][W][C]
@@ -114,6 +122,10 @@ int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const floa
 /* z = (relu)(y*scale[c] + shift[c] (+ residual)); M rows of C channels */
 int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
                   const void* residual, int relu, void* z, void* stream);
+/* z = (relu)(y*scale[c] + shift[c] + (y2*scale2[c] + shift2[c])): a block output
+ * whose residual is the downsample's BN (bn2(conv2) + bn_ds(ds)) in one pass. */
+int ssip_bn_apply2(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
+                   const void* y2, const float* scale2, const float* shift2, int relu, void* z, void* stream);
 int64_t ssip_bn_bwd_partial_floats(int64_t M, int C);
 /* dout = dz * (zmask > 0) (zmask nullable = no ReLU); dgamma/dbeta (+)= ...;
  * dy = dBN(dout); dpre (nullable) = dout.  coef: 3*C floats scratch. */
@@ -133,6 +145,17 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                               const void* y, const float* mean, const float* invstd, const float* gamma,
                               float* dgamma, float* dbeta, int accumulate, void* dy, float* coef, void* stream);
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream);
+/* Backward of z = relu(BN_a(ya) + BN_b(yb)) (ssip_bn_apply2's forward):
+ * dout = dz * (zmask > 0) feeds both BatchNorms; one reduction pass over
+ * (dz, zmask, ya, yb), one apply pass writing dy_a and dy_b (dout itself is
+ * never stored).  partial: ssip_bn_bwd_dual_partial_floats(M, C) floats;
+ * coef: 6*C floats scratch. */
+int64_t ssip_bn_bwd_dual_partial_floats(int64_t M, int C);
+int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* ya,
+                     const float* mean_a, const float* invstd_a, const float* gamma_a, float* dgamma_a,
+                     float* dbeta_a, const void* yb, const float* mean_b, const float* invstd_b,
+                     const float* gamma_b, float* dgamma_b, float* dbeta_b, int accumulate, void* dy_a, void* dy_b,
+                     float* partial, float* coef, void* stream);
 
 /* ------------------------------------------------------------------------
  * Stem BN -> ReLU -> max-pool, fused (torchvision bn1/relu/maxpool).

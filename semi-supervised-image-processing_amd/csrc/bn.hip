@@ -86,25 +86,33 @@ __global__ void bn_eval_coeffs_kernel(int C, const float* gamma, const float* be
 // stride is a multiple of C/8 (blockDim 256, C/8 | 256), so each thread keeps
 // one channel chunk and its scale/shift in registers; the grid is sized so a
 // thread handles several vectors (the per-channel loads are amortised), two
-// of them in flight per iteration.
-template <typename T>
+// of them in flight per iteration.  DUAL: the residual is itself a BatchNorm
+// output, res*scale2 + shift2, formed in registers (ssip_bn_apply2).
+template <typename T, bool DUAL>
 __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const T* __restrict__ y,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const T* __restrict__ res,
-                                                       int relu, T* __restrict__ z) {
+                                                       const float* __restrict__ scale2,
+                                                       const float* __restrict__ shift2, int relu,
+                                                       T* __restrict__ z) {
   const int cpr = C >> 3;
   const int start = blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (start % cpr) * 8;
-  float sc[8], sh[8];
+  float sc[8], sh[8], sc2[8], sh2[8];
   load_f8(sc, scale + c0);
   load_f8(sh, shift + c0);
+  if constexpr (DUAL) {
+    load_f8(sc2, scale2 + c0);
+    load_f8(sh2, shift2 + c0);
+  }
   const int stride = gridDim.x * blockDim.x;
   auto one = [&](const Vec8<T>& v, const Vec8<T>& r, int i) {
     Vec8<T> o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = __builtin_fmaf(v.get(j), sc[j], sh[j]);  // the stem's fused kernels repeat this exactly
-      if (res) t += r.get(j);
+      if constexpr (DUAL) t += __builtin_fmaf(r.get(j), sc2[j], sh2[j]);
+      else if (res) t += r.get(j);
       if (relu) t = t > 0.f ? t : 0.f;
       o.set(j, t);
     }
@@ -185,6 +193,148 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, co
   }
 }
 
+// Backward of z = relu(BN_a(ya) + BN_b(yb)): dout = dz * (zmask > 0) is the
+// gradient of both BN outputs.  Per-(row block, channel) sums of dout,
+// dout*xhat_a and dout*xhat_b, written as two [C][blocks][2] partial sets
+// (sum dout duplicated) that the ordinary finalize consumes.
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, int rows_per_block,
+                                                                 const T* __restrict__ dz,
+                                                                 const T* __restrict__ zmask,
+                                                                 const T* __restrict__ ya, const T* __restrict__ yb,
+                                                                 const float* __restrict__ mean_a,
+                                                                 const float* __restrict__ invstd_a,
+                                                                 const float* __restrict__ mean_b,
+                                                                 const float* __restrict__ invstd_b,
+                                                                 float* __restrict__ partial_a,
+                                                                 float* __restrict__ partial_b) {
+  const int cpr = C / 8;
+  const int rpi = 256 / cpr;
+  const int chunk = threadIdx.x % cpr;
+  const int rsub = threadIdx.x / cpr;
+  const int c0 = chunk * 8;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  long r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+  float sd[8], sa[8], sb[8], mua[8], isa[8], mub[8], isb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sd[j] = 0.f; sa[j] = 0.f; sb[j] = 0.f; }
+  load_f8(mua, mean_a + c0);
+  load_f8(isa, invstd_a + c0);
+  load_f8(mub, mean_b + c0);
+  load_f8(isb, invstd_b + c0);
+  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& a, const Vec8<T>& b) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = zz.get(j) > 0.f ? g.get(j) : 0.f;
+      sd[j] += d;
+      sa[j] += d * ((a.get(j) - mua[j]) * isa[j]);
+      sb[j] += d * ((b.get(j) - mub[j]) * isb[j]);
+    }
+  };
+  if (rsub < rpi) {
+    long r = r0 + rsub;
+    for (; r + rpi < r1; r += 2 * rpi) {
+      Vec8<T> g0, g1, z0, z1, a0, a1, b0, b1;
+      g0.load(dz + r * C + c0);
+      g1.load(dz + (r + rpi) * C + c0);
+      z0.load(zmask + r * C + c0);
+      z1.load(zmask + (r + rpi) * C + c0);
+      a0.load(ya + r * C + c0);
+      a1.load(ya + (r + rpi) * C + c0);
+      b0.load(yb + r * C + c0);
+      b1.load(yb + (r + rpi) * C + c0);
+      acc(g0, z0, a0, b0);
+      acc(g1, z1, a1, b1);
+    }
+    if (r < r1) {
+      Vec8<T> g0, z0, a0, b0;
+      g0.load(dz + r * C + c0);
+      z0.load(zmask + r * C + c0);
+      a0.load(ya + r * C + c0);
+      b0.load(yb + r * C + c0);
+      acc(g0, z0, a0, b0);
+    }
+  }
+  __shared__ float red[3][256][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x][j] = sd[j];
+    red[1][threadIdx.x][j] = sa[j];
+    red[2][threadIdx.x][j] = sb[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < cpr) {
+    const long o = ((long)c0 * gridDim.x + blockIdx.x) * 2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float d = 0.f, a = 0.f, b = 0.f;
+      for (int s2 = 0; s2 < rpi; ++s2) {
+        d += red[0][s2 * cpr + threadIdx.x][j];
+        a += red[1][s2 * cpr + threadIdx.x][j];
+        b += red[2][s2 * cpr + threadIdx.x][j];
+      }
+      const long oj = o + (long)j * gridDim.x * 2;
+      partial_a[oj] = d;
+      partial_a[oj + 1] = a;
+      partial_b[oj] = d;
+      partial_b[oj + 1] = b;
+    }
+  }
+}
+
+struct BnDualFin {
+  const float *partial[2], *gamma[2], *mean[2], *invstd[2];
+  float *dgamma[2], *dbeta[2], *coef[2];
+};
+
+// both finalizes in one launch: workgroup c < C for BN a, C + c for BN b
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_dual_kernel(int C, int blocks, long M, BnDualFin f,
+                                                                    int accumulate) {
+  __shared__ double sh[2 * 16];
+  const int s = blockIdx.x >= C ? 1 : 0;
+  const int c = blockIdx.x - s * C;
+  bn_bwd_finalize_body(c, C, blocks, M, 1, s ? f.partial[1] : f.partial[0], s ? f.gamma[1] : f.gamma[0],
+                       s ? f.mean[1] : f.mean[0], s ? f.invstd[1] : f.invstd[0], s ? f.dgamma[1] : f.dgamma[0],
+                       s ? f.dbeta[1] : f.dbeta[0], accumulate, s ? f.coef[1] : f.coef[0], sh);
+}
+
+// dy_a = A_a*dout + B_a*ya + C_a,  dy_b = A_b*dout + B_b*yb + C_b
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(int total8, int C, const T* __restrict__ dz,
+                                                                const T* __restrict__ zmask,
+                                                                const T* __restrict__ ya, const T* __restrict__ yb,
+                                                                const float* __restrict__ coef_a,
+                                                                const float* __restrict__ coef_b,
+                                                                T* __restrict__ dya, T* __restrict__ dyb) {
+  const int cpr = C >> 3;
+  const int start = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (start % cpr) * 8;
+  float aa[8], ab[8], ac[8], ba[8], bb[8], bc[8];
+  load_f8(aa, coef_a + c0);
+  load_f8(ab, coef_a + C + c0);
+  load_f8(ac, coef_a + 2 * C + c0);
+  load_f8(ba, coef_b + c0);
+  load_f8(bb, coef_b + C + c0);
+  load_f8(bc, coef_b + 2 * C + c0);
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = start; i < total8; i += stride) {
+    Vec8<T> g, zz, a, b, oa, ob;
+    g.load(dz + (long)i * 8);
+    zz.load(zmask + (long)i * 8);
+    a.load(ya + (long)i * 8);
+    b.load(yb + (long)i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = zz.get(j) > 0.f ? g.get(j) : 0.f;
+      oa.set(j, aa[j] * d + ab[j] * a.get(j) + ac[j]);
+      ob.set(j, ba[j] * d + bb[j] * b.get(j) + bc[j]);
+    }
+    oa.store(dya + (long)i * 8);
+    ob.store(dyb + (long)i * 8);
+  }
+}
+
 // dst = src * (mask > 0)  (ReLU backward as a standalone pass)
 template <typename T>
 __global__ void relu_bwd_kernel(long total8, const T* __restrict__ g, const T* __restrict__ z, T* __restrict__ out) {
@@ -247,10 +397,64 @@ int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply: unsupported size");
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream, total8, C,
-                       (const T*)y, scale, shift, (const T*)residual, relu, (T*)z);
+    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
+                       total8, C, (const T*)y, scale, shift, (const T*)residual, (const float*)nullptr,
+                       (const float*)nullptr, relu, (T*)z);
   });
   return ::ssip::check_launch("bn_apply");
+}
+
+int ssip_bn_apply2(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
+                   const void* y2, const float* scale2, const float* shift2, int relu, void* z, void* stream) {
+  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && y && scale && shift && y2 && scale2 && shift2 && z, SSIP_ERR_ARG,
+               "ssip_bn_apply2: bad arguments");
+  SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply2: unsupported size");
+  const int total8 = (int)(M * C / 8);
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
+                       total8, C, (const T*)y, scale, shift, (const T*)y2, scale2, shift2, relu, (T*)z);
+  });
+  return ::ssip::check_launch("bn_apply2");
+}
+
+int64_t ssip_bn_bwd_dual_partial_floats(int64_t M, int C) {
+  const int64_t n = ssip_bn_bwd_partial_floats(M, C);
+  return n < 0 ? n : 2 * n;
+}
+
+int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* ya,
+                     const float* mean_a, const float* invstd_a, const float* gamma_a, float* dgamma_a,
+                     float* dbeta_a, const void* yb, const float* mean_b, const float* invstd_b,
+                     const float* gamma_b, float* dgamma_b, float* dbeta_b, int accumulate, void* dy_a, void* dy_b,
+                     float* partial, float* coef, void* stream) {
+  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= 2048 && dz && zmask && ya && yb && mean_a && invstd_a &&
+                   mean_b && invstd_b && dy_a && dy_b && partial && coef,
+               SSIP_ERR_ARG, "ssip_bn_bwd_dual: bad arguments");
+  SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_bwd_dual: unsupported size");
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = bwd_rows_per_block(M, C);
+  const int blocks = (int)((M + rows - 1) / rows);
+  const int total8 = (int)(M * C / 8);
+  float* pa = partial;
+  float* pb = partial + (long)blocks * C * 2;
+  BnDualFin f;
+  f.partial[0] = pa; f.partial[1] = pb;
+  f.gamma[0] = gamma_a; f.gamma[1] = gamma_b;
+  f.mean[0] = mean_a; f.mean[1] = mean_b;
+  f.invstd[0] = invstd_a; f.invstd[1] = invstd_b;
+  f.dgamma[0] = dgamma_a; f.dgamma[1] = dgamma_b;
+  f.dbeta[0] = dbeta_a; f.dbeta[1] = dbeta_b;
+  f.coef[0] = coef; f.coef[1] = coef + 3 * C;
+  SSIP_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(bn_bwd_reduce_dual_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
+                       (const T*)zmask, (const T*)ya, (const T*)yb, mean_a, invstd_a, mean_b, invstd_b, pa, pb);
+    hipLaunchKernelGGL(bn_bwd_finalize_dual_kernel, dim3(2 * C), dim3(1024), 0, st, C, blocks, (long)M, f,
+                       accumulate);
+    hipLaunchKernelGGL(bn_bwd_apply_dual_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
+                       (const T*)dz, (const T*)zmask, (const T*)ya, (const T*)yb, coef, coef + 3 * C, (T*)dy_a,
+                       (T*)dy_b);
+  });
+  return ::ssip::check_launch("bn_bwd_dual");
 }
 
 int64_t ssip_bn_bwd_partial_floats(int64_t M, int C) {

@@ -32,14 +32,11 @@ __device__ __forceinline__ void block_sums_f64_1024(double (&v)[V], double* sh) 
 // One 1024-thread workgroup per channel: sums of dout and dout*xhat over the
 // partials (threads take blocks t = tid, tid + 1024, ...); cmajor: [C][blocks][2]
 // (each channel's records contiguous), else [blocks][C][2].
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int C, int blocks, long M, int cmajor,
-                                                               const float* __restrict__ partial,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ mean,
-                                                               const float* __restrict__ invstd, float* dgamma,
-                                                               float* dbeta, int accumulate, float* coef) {
-  __shared__ double sh[2 * 16];
-  const int c = blockIdx.x;
+__device__ __forceinline__ void bn_bwd_finalize_body(int c, int C, int blocks, long M, int cmajor,
+                                                     const float* __restrict__ partial,
+                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd, float* dgamma, float* dbeta,
+                                                     int accumulate, float* coef, double* sh) {
   double ab[2] = {0.0, 0.0};
   const long cs = cmajor ? 2 : (long)C * 2;
   const float* pc = partial + (cmajor ? (long)c * blocks * 2 : (long)c * 2);
@@ -61,6 +58,17 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int C, int blocks
     coef[C + c] = (float)k1;                      // * y
     coef[2 * C + c] = (float)(k0 - k1 * mean[c]);  // constant
   }
+}
+
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int C, int blocks, long M, int cmajor,
+                                                               const float* __restrict__ partial,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd, float* dgamma,
+                                                               float* dbeta, int accumulate, float* coef) {
+  __shared__ double sh[2 * 16];
+  bn_bwd_finalize_body(blockIdx.x, C, blocks, M, cmajor, partial, gamma, mean, invstd, dgamma, dbeta, accumulate,
+                       coef, sh);
 }
 
 static inline int bn_bwd_finalize_grid(int C) { return C; }

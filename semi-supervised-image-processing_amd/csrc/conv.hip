@@ -26,6 +26,7 @@
 // batch statistics need no extra pass over Y.  WGRAD is split over the m
 // reduction into fp32 slabs that a second kernel sums in fixed order
 // (bitwise reproducible, no atomics).
+#include <algorithm>
 #include "ssip_common.h"
 
 namespace {
@@ -83,6 +84,18 @@ struct ConvArgs {
   // r = r0 + 2*ri, s = s0 + 2*si reach them, at dy row p = i + bh - ri.
   int phased;
   PhaseInfo phase[4];
+  // phase order (2 bits each, heaviest first): workgroup t of an XCD's
+  // contiguous run takes phase (phase_order >> 2*(t & 3)) & 3 of tile t >> 2,
+  // so every XCD gets the same mix of long and short phases
+  int phase_order;
+  // DGRAD of a stride-2 3x3 conv fused with its block's 1x1 / stride-2
+  // downsample (ssip_conv_dgrad_ds): phase (0, 0) -- the only one the
+  // downsample reaches, at the same dy pixel as its single tap -- runs
+  // ds_from own k-steps, then K/64 more over dY_ds (A2) and W_ds [C][K] (B2)
+  const void* A2;
+  const void* B2;
+  uint32_t a2_bytes, b2_bytes;
+  int ds_from;
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
   uint32_t a_bytes, b_bytes;  // operand extents (LDS-DMA kernel buffer resources)
   // WGRAD x-gather walk: a 64-row k-step advances each row's output pixel
@@ -888,8 +901,13 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
     const int lin = blockIdx.x + blockIdx.y * gridDim.x;
     const int xcd = lin & 7, q = nb >> 3, r = nb & 7;
     const int t = a.xcd_remap ? xcd * q + min(xcd, r) + (lin >> 3) : lin;
-    bx = t % gridDim.x;
-    by = t / gridDim.x;
+    if (MODE == MODE_DGRAD && a.phased) {  // gridDim.y == 4: all phases of a tile together, heaviest first
+      bx = t >> 2;
+      by = (a.phase_order >> (2 * (t & 3))) & 3;
+    } else {
+      bx = t % gridDim.x;
+      by = t / gridDim.x;
+    }
   }
   const int tn = bx % a.tiles_n;
   const int tm = bx / a.tiles_n;
@@ -1028,6 +1046,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   constexpr bool BUF_A = !C4;
   uint32_t a_off[LA], a_msk[LA], b_off[LB];
   __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ag, a.a_bytes), rsB = make_rsrc(Bg, a.b_bytes);
+  const bool dsx = (MODE == MODE_DGRAD) && phased && f == 0 && a.A2 != nullptr;
   if constexpr (!WG && BUF_A) {
     const int nr = phased ? ph_nr : a.R, ns = phased ? ph_ns : a.S;
 #pragma unroll
@@ -1112,6 +1131,18 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
         blds16(rsA, ok ? a_off[t] + toff : SSIP_OOB, As + (wave + NW * t) * 1024);
       }
     } else if constexpr (MODE == MODE_DGRAD) {
+      if (dsx && ks == a.ds_from) {
+        // switch to the fused downsample: its dY_ds pixel is this phase's tap-0
+        // pixel (same a_off / mask bit 0), its weights are [C][K]
+        rsA = make_rsrc(a.A2, a.a2_bytes);
+        rsB = make_rsrc(a.B2, a.b2_bytes);
+#pragma unroll
+        for (int t = 0; t < LB; ++t) {
+          const int row = 8 * (wave + NW * t) + (lane >> 3);
+          b_off[t] = b_ok[t] ? (uint32_t)(((long)(n0 + row) * a.K + b_c[t] * 8) * 2) : 0xF0000000u;
+        }
+        kr = 0; ks_ = 0; kcb = 0; ph_r0 = 0; ph_s0 = 0; ph_ns = 1;
+      }
       const int tp = kr * ph_ns + ks_;
       const uint32_t toff = (uint32_t)((kcb - (kr * a.Q + ks_) * a.K) * 2);
 #pragma unroll
@@ -2641,6 +2672,14 @@ static void fallback_regstaged(Plan& pl) {
   pl.grid = dim3(ceil_div(a.M, pl.bm) * a.tiles_n, 1, 1);
 }
 
+// phases by k-steps, descending (ties in phase order): the kernel hands them
+// out in this order within each tile, so the long phases start first
+static void set_phase_order(ConvArgs& a) {
+  int ord[4] = {0, 1, 2, 3};
+  std::stable_sort(ord, ord + 4, [&](int x, int y) { return a.phase[x].ksteps > a.phase[y].ksteps; });
+  a.phase_order = ord[0] | (ord[1] << 2) | (ord[2] << 4) | (ord[3] << 6);
+}
+
 // Stride-2 DGRAD as four dense sub-problems, one per output parity phase:
 // phase (ph, pw) only meets the taps r = r0 + 2*ri, s = s0 + 2*si, so the
 // k-loop skips the 3/4 of (tap, pixel) pairs the plain implicit GEMM would
@@ -2671,6 +2710,7 @@ static void phase_split(Plan& pl, const ssip_conv_desc* d) {
     max_tiles = std::max(max_tiles, P.tiles_m);
   }
   a.phased = 1;
+  set_phase_order(a);
   pl.grid = dim3(std::max(1, max_tiles) * a.tiles_n, 4, 1);
 }
 
@@ -2892,6 +2932,41 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));
+}
+
+int ssip_conv_dgrad_ds(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dy_ds,
+                       const void* wds_ck, void* dx, void* stream) {
+  SSIP_REQUIRE(desc_ok(d) && dy && w_crsk && dy_ds && wds_ck && dx, SSIP_ERR_ARG, "ssip_conv_dgrad_ds: bad arguments");
+  SSIP_REQUIRE(d->H % d->stride == 0 && d->W % d->stride == 0 && d->P * d->stride == d->H &&
+                   d->Q * d->stride == d->W, SSIP_ERR_ARG,
+               "ssip_conv_dgrad_ds: the 1x1 downsample's output grid must equal the conv's (H, W divisible by stride)");
+  ssip_conv_desc dd = *d;  // the block's 1x1 / stride downsample: same input, same output grid
+  dd.R = 1; dd.S = 1; dd.pad = 0;
+  Plan pl;
+  int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
+  if (rc) return rc;
+  phase_split(pl, d);
+  const bool fuse = pl.stages > 0 && pl.args.phased && d->R == 3 && d->S == 3 && d->pad == 1 && d->stride == 2 &&
+                    !getenv("SSIP_CONV_NO_DSFUSE");
+  if (!fuse) {  // two passes: the conv's dgrad, then the downsample's accumulated in place
+    rc = ssip_conv_dgrad(d, dtype, dy, w_crsk, dx, nullptr, stream);
+    if (rc) return rc;
+    return ssip_conv_dgrad(&dd, dtype, dy_ds, wds_ck, dx, dx, stream);
+  }
+  ConvArgs& a = pl.args;
+  a.A = dy; a.B = w_crsk; a.out = dx; a.add = nullptr;
+  a.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
+  a.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
+  a.A2 = dy_ds; a.B2 = wds_ck;
+  a.a2_bytes = a.a_bytes;
+  a.b2_bytes = (uint32_t)((long)d->K * d->C * 2);
+  // phase (0, 0): h = 2i, w = 2j meet tap (1, 1) at dy pixel (i, j) -- the downsample's pixel
+  SSIP_REQUIRE(a.phase[0].nr == 1 && a.phase[0].ns == 1 && a.phase[0].bh == 0 && a.phase[0].bw == 0, SSIP_ERR_ARG,
+               "ssip_conv_dgrad_ds: unexpected phase (0, 0) geometry");
+  a.ds_from = a.phase[0].ksteps;
+  a.phase[0].ksteps += d->K / 64;
+  set_phase_order(a);
+  return launch_conv<MODE_DGRAD, __bf16>(pl, (hipStream_t)stream);
 }
 
 int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d) {

@@ -29,7 +29,7 @@ def abi_version_expected() -> int:
     return int(m.group(1)) if m else ABI_VERSION
 
 
-ABI_VERSION = 4  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
+ABI_VERSION = 5  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1
@@ -83,6 +83,7 @@ _SIGS = {
     "ssip_conv_fwd_partial_tiles": (_c_int, [_PD, _c_int]),
     "ssip_conv_fwd": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_conv_dgrad_ds": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad_bn_partial_floats": (_c_i64, [_PD]),
     "ssip_conv_dgrad_bn_partial_tiles": (_c_int, [_PD, _c_int]),
     "ssip_conv_dgrad_bn": (_c_int, [_PD, _c_int] + [_vp] * 10),
@@ -94,6 +95,9 @@ _SIGS = {
     "ssip_bn_finalize": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_eval_coeffs": (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_apply": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
+    "ssip_bn_apply2": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
+    "ssip_bn_bwd_dual_partial_floats": (_c_i64, [_c_i64, _c_int]),
+    "ssip_bn_bwd_dual": (_c_int, [_c_int, _c_i64, _c_int] + [_vp] * 14 + [_c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_bwd_partial_floats": (_c_i64, [_c_i64, _c_int]),
     "ssip_bn_bwd": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_relu_bwd": (_c_int, [_c_int, _c_i64, _c_int] + [_vp] * 9 + [_c_int, _vp, _vp, _vp, _vp]),

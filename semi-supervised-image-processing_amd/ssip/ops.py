@@ -210,6 +210,22 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx: torch.Te
     call(*args)
 
 
+def conv_dgrad_ds(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, gds: ConvGeom, dy_ds: torch.Tensor,
+                  wds_crsk: torch.Tensor, dx: torch.Tensor) -> None:
+    """dx = dgrad(conv g, dy) + dgrad(1x1/stride downsample gds, dy_ds) (ssip_conv_dgrad_ds)."""
+    assert gds.R == 1 and gds.S == 1 and gds.pad == 0 and gds.stride == g.stride and (gds.P, gds.Q) == (g.P, g.Q)
+    assert (gds.N, gds.H, gds.W, gds.C, gds.K) == (g.N, g.H, g.W, g.C, g.K), "conv_dgrad_ds: geometries differ"
+    assert dy.numel() == dy_ds.numel() == g.N * g.P * g.Q * g.K, "conv_dgrad_ds: dy shape"
+    assert w_crsk.numel() == g.K * g.R * g.S * g.C and wds_crsk.numel() == g.K * g.C, "conv_dgrad_ds: w shape"
+    assert dx.numel() == g.N * g.H * g.W * g.C, "conv_dgrad_ds: dx shape"
+    args = ("ssip_conv_dgrad_ds", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dy_ds), _p(wds_crsk), _p(dx),
+            stream_ptr())
+    if _timer is not None:
+        _timer.wrap("dgrad", g.flops() + gds.flops(), call, *args)
+        return
+    call(*args)
+
+
 def conv_dgrad_bn_partial_floats(g: ConvGeom) -> int:
     return int(_lib.lib().ssip_conv_dgrad_bn_partial_floats(g.desc()))
 
@@ -320,6 +336,27 @@ def bn_eval_coeffs(C: int, gamma, beta, running_mean, running_var, eps: float, m
 def bn_apply(M: int, C: int, y, scale, shift, residual, relu: bool, z) -> None:
     call("ssip_bn_apply", dtype_code(y), M, C, _p(y), _p(scale), _p(shift), _p(residual), int(relu), _p(z),
          stream_ptr())
+
+
+def bn_apply2(M: int, C: int, y, scale, shift, y2, scale2, shift2, relu: bool, z) -> None:
+    """z = relu(y*scale + shift + y2*scale2 + shift2) (block output with a downsample BN residual)."""
+    call("ssip_bn_apply2", dtype_code(y), M, C, _p(y), _p(scale), _p(shift), _p(y2), _p(scale2), _p(shift2),
+         int(relu), _p(z), stream_ptr())
+
+
+def bn_bwd_dual_partial_floats(M: int, C: int) -> int:
+    n = int(call("ssip_bn_bwd_dual_partial_floats", M, C))
+    if n < 0:
+        raise RuntimeError(f"ssip_bn_bwd_dual_partial_floats({M}, {C}) unsupported")
+    return n
+
+
+def bn_bwd_dual(M: int, C: int, dz, zmask, ya, mean_a, invstd_a, gamma_a, dgamma_a, dbeta_a, yb, mean_b, invstd_b,
+                gamma_b, dgamma_b, dbeta_b, accumulate: bool, dy_a, dy_b, partial, coef) -> None:
+    """Backward of z = relu(BN_a(ya) + BN_b(yb)) (ssip_bn_bwd_dual); coef: 6*C floats."""
+    call("ssip_bn_bwd_dual", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(ya), _p(mean_a), _p(invstd_a), _p(gamma_a),
+         _p(dgamma_a), _p(dbeta_a), _p(yb), _p(mean_b), _p(invstd_b), _p(gamma_b), _p(dgamma_b), _p(dbeta_b),
+         int(accumulate), _p(dy_a), _p(dy_b), _p(partial), _p(coef), stream_ptr())
 
 
 def bn_bwd_partial_floats(M: int, C: int) -> int:

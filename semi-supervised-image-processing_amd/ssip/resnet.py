@@ -408,14 +408,15 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
             recs.append(r)
         last = recs[-1]
         ds = None
-        if blk.downsample is not None:
-            ds = _conv_bn(model, blk.downsample[0], blk.downsample[1], x, N, Hc, Wc, train, save, upd)
-            ident = torch.empty_like(ds.y)
-            ops.bn_apply(N * h * w, ds.geom.K, ds.y, ds.stats[2], ds.stats[3], None, False, ident)
-        else:
-            ident = x
         out = torch.empty_like(last.y)
-        ops.bn_apply(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], ident, True, out)
+        if blk.downsample is not None:
+            # out = relu(bn2(y2) + bn_ds(y_ds)): the downsample's BN is formed in
+            # registers by the same pass (its output is never stored)
+            ds = _conv_bn(model, blk.downsample[0], blk.downsample[1], x, N, Hc, Wc, train, save, upd)
+            ops.bn_apply2(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], ds.y, ds.stats[2],
+                          ds.stats[3], True, out)
+        else:
+            ops.bn_apply(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], x, True, out)
         last.z = out
         if save:
             sv.blocks.append((recs, ds, x))
@@ -568,7 +569,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(r.geom))
     ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(sv.stem.geom))
     workspace = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
-    coef_buf = torch.empty(3 * 2048, device=dev, dtype=torch.float32)
+    coef_buf = torch.empty(6 * 2048, device=dev, dtype=torch.float32)
 
     def bn_grads(rec: _ConvRec):
         bn = rec.bn
@@ -617,6 +618,25 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                                  rec.bn.weight.detach(), dgam, dbet, acc, dy, coef_buf[: 3 * g.K])
         return dy
 
+    def bn_backward_dual(rec_a: _ConvRec, rec_b: _ConvRec, dzin, zmask):
+        """Backward of z = relu(BN_a(y_a) + BN_b(y_b)) in one reduction and one
+        apply pass (the masked gradient that feeds both is never stored);
+        None when the two BNs' gradients do not both accumulate or both start fresh."""
+        g = rec_a.geom
+        M = N * g.P * g.Q
+        ga, ba, acc_a = bn_grads(rec_a)
+        gb, bb, acc_b = bn_grads(rec_b)
+        if (ga is not None or ba is not None) and (gb is not None or bb is not None) and acc_a != acc_b:
+            return None
+        acc = acc_a if (ga is not None or ba is not None) else acc_b
+        dya = torch.empty_like(rec_a.y)
+        dyb = torch.empty_like(rec_b.y)
+        partial = torch.empty(ops.bn_bwd_dual_partial_floats(M, g.K), device=dev, dtype=torch.float32)
+        ops.bn_bwd_dual(M, g.K, dzin, zmask, rec_a.y, rec_a.stats[0], rec_a.stats[1], rec_a.bn.weight.detach(), ga,
+                        ba, rec_b.y, rec_b.stats[0], rec_b.stats[1], rec_b.bn.weight.detach(), gb, bb, acc, dya, dyb,
+                        partial, coef_buf[: 6 * g.K])
+        return dya, dyb
+
     def conv_wgrad(rec: _ConvRec, dy):
         w = rec.conv.weight
         if not w.requires_grad:
@@ -656,17 +676,23 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         need_dx = first_trainable is not None and first_trainable < stage_idx
         below = sv.blocks[bi - 1][0][-1] if bi > 0 else None  # BN+ReLU producing this block's input
         last = recs[-1]
-        if pending is None:
-            dpre = torch.empty_like(last.y)
-            dy = bn_backward(last, dz, last.z, dpre)
+        dual = None
+        if pending is None and ds is not None:
+            dual = bn_backward_dual(last, ds, dz, last.z)
+        dpre = None
+        if dual is not None:
+            dy, dy_ds = dual
         else:
-            dpre, part, tiles = pending
-            dy = bn_backward_fused(last, dpre, part, tiles)
+            if pending is None:
+                dpre = torch.empty_like(last.y)
+                dy = bn_backward(last, dz, last.z, dpre)
+            else:
+                dpre, part, tiles = pending
+                dy = bn_backward_fused(last, dpre, part, tiles)
+            dy_ds = bn_backward(ds, dpre, None) if ds is not None else None
         pending = None
-        dy_ds = None
-        if ds is not None:
-            dy_ds = bn_backward(ds, dpre, None)
         # main path, last conv back to the first
+        ds_dgrad_done = False
         g_cur = dy
         dxin = None
         for i in range(len(recs) - 1, -1, -1):
@@ -685,11 +711,16 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                     pending = conv_dgrad_bn(r, g_cur, below, dxin, dpre)
                 elif ds is None:
                     conv_dgrad(r, g_cur, dxin, dpre)
+                elif _ds_dgrad_fusable(r.geom, ds.geom) and (below is None or not _FUSE_BN_BWD):
+                    # conv1's and the downsample's input gradients in one launch
+                    ops.conv_dgrad_ds(r.geom, g_cur, _prepped_t(model, r)[1], ds.geom, dy_ds,
+                                      _prepped_t(model, ds)[1], dxin)
+                    ds_dgrad_done = True
                 else:
                     conv_dgrad(r, g_cur, dxin)
         if ds is not None:
             conv_wgrad(ds, dy_ds)
-            if dxin is not None:
+            if dxin is not None and not ds_dgrad_done:
                 if below is not None:
                     pending = conv_dgrad_bn(ds, dy_ds, below, dxin, dxin)
                 else:
@@ -733,6 +764,13 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         conv_wgrad(stem, dy1)
     if hook is not None:
         hook([model.conv1.weight, model.bn1.weight, model.bn1.bias])
+
+
+def _ds_dgrad_fusable(g: ConvGeom, gds: ConvGeom) -> bool:
+    """conv1 and the downsample of a block read the same input and produce the
+    same output grid (BasicBlock): ssip_conv_dgrad_ds takes both."""
+    return (gds.R == 1 and gds.S == 1 and gds.pad == 0 and gds.stride == g.stride
+            and (g.N, g.H, g.W, g.C, g.K, g.P, g.Q) == (gds.N, gds.H, gds.W, gds.C, gds.K, gds.P, gds.Q))
 
 
 def _prepped_t(model: SSIPResNet, rec: _ConvRec):

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 5
+#define SSIP_ABI_VERSION 6
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -119,17 +119,22 @@ int ssip_bn_finalize(int C, int tiles, const float* partial, const float* gamma,
 int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
                         const float* running_var, float eps, float* mean_out, float* invstd_out, float* scale_out,
                         float* shift_out, void* stream);
-/* z = (relu)(y*scale[c] + shift[c] (+ residual)); M rows of C channels */
+/* z = (relu)(y*scale[c] + shift[c] (+ residual)); M rows of C channels.
+ * mask_bits (nullable): bit j of byte i = (z[8i + j] > 0), the ReLU mask the
+ * backward reads instead of z (1/16 of its bytes in bf16). */
 int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
-                  const void* residual, int relu, void* z, void* stream);
+                  const void* residual, int relu, void* z, uint8_t* mask_bits, void* stream);
 /* z = (relu)(y*scale[c] + shift[c] + (y2*scale2[c] + shift2[c])): a block output
  * whose residual is the downsample's BN (bn2(conv2) + bn_ds(ds)) in one pass. */
 int ssip_bn_apply2(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
-                   const void* y2, const float* scale2, const float* shift2, int relu, void* z, void* stream);
+                   const void* y2, const float* scale2, const float* shift2, int relu, void* z, uint8_t* mask_bits,
+                   void* stream);
 int64_t ssip_bn_bwd_partial_floats(int64_t M, int C);
-/* dout = dz * (zmask > 0) (zmask nullable = no ReLU); dgamma/dbeta (+)= ...;
- * dy = dBN(dout); dpre (nullable) = dout.  coef: 3*C floats scratch. */
-int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
+/* dout = dz * (zmask > 0), or * mask bit (mask_bits as ssip_bn_apply writes them);
+ * both NULL = no ReLU; dgamma/dbeta (+)= ...; dy = dBN(dout); dpre (nullable)
+ * = dout.  coef: 3*C floats scratch. */
+int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mask_bits,
+                const void* y, const float* mean,
                 const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
                 void* dpre, float* partial, float* coef, void* stream);
 /* ssip_bn_bwd for a BN+ReLU without residual: the ReLU mask is recomputed
@@ -146,12 +151,13 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                               float* dgamma, float* dbeta, int accumulate, void* dy, float* coef, void* stream);
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream);
 /* Backward of z = relu(BN_a(ya) + BN_b(yb)) (ssip_bn_apply2's forward):
- * dout = dz * (zmask > 0) feeds both BatchNorms; one reduction pass over
- * (dz, zmask, ya, yb), one apply pass writing dy_a and dy_b (dout itself is
+ * dout = dz * (zmask > 0) (or the mask bits) feeds both BatchNorms; one
+ * reduction pass over (dz, mask, ya, yb), one apply pass writing dy_a and dy_b (dout itself is
  * never stored).  partial: ssip_bn_bwd_dual_partial_floats(M, C) floats;
  * coef: 6*C floats scratch. */
 int64_t ssip_bn_bwd_dual_partial_floats(int64_t M, int C);
-int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* ya,
+int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mask_bits,
+                     const void* ya,
                      const float* mean_a, const float* invstd_a, const float* gamma_a, float* dgamma_a,
                      float* dbeta_a, const void* yb, const float* mean_b, const float* invstd_b,
                      const float* gamma_b, float* dgamma_b, float* dbeta_b, int accumulate, void* dy_a, void* dy_b,

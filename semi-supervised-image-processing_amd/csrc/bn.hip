@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const 
                                                        const float* __restrict__ shift, const T* __restrict__ res,
                                                        const float* __restrict__ scale2,
                                                        const float* __restrict__ shift2, int relu,
-                                                       T* __restrict__ z) {
+                                                       T* __restrict__ z, uint8_t* __restrict__ mbits) {
   const int cpr = C >> 3;
   const int start = blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (start % cpr) * 8;
@@ -108,6 +108,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const 
   const int stride = gridDim.x * blockDim.x;
   auto one = [&](const Vec8<T>& v, const Vec8<T>& r, int i) {
     Vec8<T> o;
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = __builtin_fmaf(v.get(j), sc[j], sh[j]);  // the stem's fused kernels repeat this exactly
@@ -115,8 +116,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const 
       else if (res) t += r.get(j);
       if (relu) t = t > 0.f ? t : 0.f;
       o.set(j, t);
+      bits |= (o.get(j) > 0.f ? 1u : 0u) << j;  // the stored value's sign: the backward's ReLU mask
     }
     o.store(z + (long)i * 8);
+    if (mbits) mbits[i] = (uint8_t)bits;
   };
   int i = start;
   for (; i + stride < total8; i += 2 * stride) {
@@ -140,7 +143,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(int total8, int C, const 
 
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, const T* __restrict__ dz,
-                                                           const T* __restrict__ zmask, const T* __restrict__ y,
+                                                           const T* __restrict__ zmask,
+                                                           const uint8_t* __restrict__ mbits, const T* __restrict__ y,
                                                            const float* __restrict__ coef, T* __restrict__ dy,
                                                            T* __restrict__ dpre, const float* __restrict__ mscale,
                                                            const float* __restrict__ mshift) {
@@ -159,11 +163,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, co
   const int stride = gridDim.x * blockDim.x;
   auto one = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& yy, int i) {
     Vec8<T> o, p;
+    const uint32_t mb = mbits ? mbits[i] : 0xFFu;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float d = g.get(j);
       if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
       if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
+      d = ((mb >> j) & 1u) ? d : 0.f;
       p.set(j, d);
       o.set(j, ca[j] * d + cb[j] * yy.get(j) + cc[j]);
     }
@@ -201,6 +207,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, int rows_per_block,
                                                                  const T* __restrict__ dz,
                                                                  const T* __restrict__ zmask,
+                                                                 const uint8_t* __restrict__ mbits,
                                                                  const T* __restrict__ ya, const T* __restrict__ yb,
                                                                  const float* __restrict__ mean_a,
                                                                  const float* __restrict__ invstd_a,
@@ -223,10 +230,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, 
   load_f8(isa, invstd_a + c0);
   load_f8(mub, mean_b + c0);
   load_f8(isb, invstd_b + c0);
-  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& a, const Vec8<T>& b) {
+  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, uint32_t mb, const Vec8<T>& a, const Vec8<T>& b) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d = zz.get(j) > 0.f ? g.get(j) : 0.f;
+      const bool on = mbits ? ((mb >> j) & 1u) != 0 : zz.get(j) > 0.f;
+      const float d = on ? g.get(j) : 0.f;
       sd[j] += d;
       sa[j] += d * ((a.get(j) - mua[j]) * isa[j]);
       sb[j] += d * ((b.get(j) - mub[j]) * isb[j]);
@@ -236,24 +244,32 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, 
     long r = r0 + rsub;
     for (; r + rpi < r1; r += 2 * rpi) {
       Vec8<T> g0, g1, z0, z1, a0, a1, b0, b1;
+      uint32_t m0 = 0, m1 = 0;
       g0.load(dz + r * C + c0);
       g1.load(dz + (r + rpi) * C + c0);
-      z0.load(zmask + r * C + c0);
-      z1.load(zmask + (r + rpi) * C + c0);
+      if (mbits) {
+        m0 = mbits[r * cpr + chunk];
+        m1 = mbits[(r + rpi) * cpr + chunk];
+      } else {
+        z0.load(zmask + r * C + c0);
+        z1.load(zmask + (r + rpi) * C + c0);
+      }
       a0.load(ya + r * C + c0);
       a1.load(ya + (r + rpi) * C + c0);
       b0.load(yb + r * C + c0);
       b1.load(yb + (r + rpi) * C + c0);
-      acc(g0, z0, a0, b0);
-      acc(g1, z1, a1, b1);
+      acc(g0, z0, m0, a0, b0);
+      acc(g1, z1, m1, a1, b1);
     }
     if (r < r1) {
       Vec8<T> g0, z0, a0, b0;
+      uint32_t m0 = 0;
       g0.load(dz + r * C + c0);
-      z0.load(zmask + r * C + c0);
+      if (mbits) m0 = mbits[r * cpr + chunk];
+      else z0.load(zmask + r * C + c0);
       a0.load(ya + r * C + c0);
       b0.load(yb + r * C + c0);
-      acc(g0, z0, a0, b0);
+      acc(g0, z0, m0, a0, b0);
     }
   }
   __shared__ float red[3][256][9];
@@ -303,6 +319,7 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_dual_kernel(int C, int b
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(int total8, int C, const T* __restrict__ dz,
                                                                 const T* __restrict__ zmask,
+                                                                const uint8_t* __restrict__ mbits,
                                                                 const T* __restrict__ ya, const T* __restrict__ yb,
                                                                 const float* __restrict__ coef_a,
                                                                 const float* __restrict__ coef_b,
@@ -320,13 +337,16 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(int total8, int 
   const int stride = gridDim.x * blockDim.x;
   for (int i = start; i < total8; i += stride) {
     Vec8<T> g, zz, a, b, oa, ob;
+    uint32_t mb = 0;
     g.load(dz + (long)i * 8);
-    zz.load(zmask + (long)i * 8);
+    if (mbits) mb = mbits[i];
+    else zz.load(zmask + (long)i * 8);
     a.load(ya + (long)i * 8);
     b.load(yb + (long)i * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d = zz.get(j) > 0.f ? g.get(j) : 0.f;
+      const bool on = mbits ? ((mb >> j) & 1u) != 0 : zz.get(j) > 0.f;
+      const float d = on ? g.get(j) : 0.f;
       oa.set(j, aa[j] * d + ab[j] * a.get(j) + ac[j]);
       ob.set(j, ba[j] * d + bb[j] * b.get(j) + bc[j]);
     }
@@ -392,27 +412,28 @@ int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const floa
 }
 
 int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
-                  const void* residual, int relu, void* z, void* stream) {
+                  const void* residual, int relu, void* z, uint8_t* mask_bits, void* stream) {
   SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && y && scale && shift && z, SSIP_ERR_ARG, "ssip_bn_apply: bad arguments");
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply: unsupported size");
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
                        total8, C, (const T*)y, scale, shift, (const T*)residual, (const float*)nullptr,
-                       (const float*)nullptr, relu, (T*)z);
+                       (const float*)nullptr, relu, (T*)z, mask_bits);
   });
   return ::ssip::check_launch("bn_apply");
 }
 
 int ssip_bn_apply2(int dtype, int64_t M, int C, const void* y, const float* scale, const float* shift,
-                   const void* y2, const float* scale2, const float* shift2, int relu, void* z, void* stream) {
+                   const void* y2, const float* scale2, const float* shift2, int relu, void* z, uint8_t* mask_bits,
+                   void* stream) {
   SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && y && scale && shift && y2 && scale2 && shift2 && z, SSIP_ERR_ARG,
                "ssip_bn_apply2: bad arguments");
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply2: unsupported size");
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
-                       total8, C, (const T*)y, scale, shift, (const T*)y2, scale2, shift2, relu, (T*)z);
+                       total8, C, (const T*)y, scale, shift, (const T*)y2, scale2, shift2, relu, (T*)z, mask_bits);
   });
   return ::ssip::check_launch("bn_apply2");
 }
@@ -422,12 +443,13 @@ int64_t ssip_bn_bwd_dual_partial_floats(int64_t M, int C) {
   return n < 0 ? n : 2 * n;
 }
 
-int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* ya,
+int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mask_bits,
+                     const void* ya,
                      const float* mean_a, const float* invstd_a, const float* gamma_a, float* dgamma_a,
                      float* dbeta_a, const void* yb, const float* mean_b, const float* invstd_b,
                      const float* gamma_b, float* dgamma_b, float* dbeta_b, int accumulate, void* dy_a, void* dy_b,
                      float* partial, float* coef, void* stream) {
-  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= 2048 && dz && zmask && ya && yb && mean_a && invstd_a &&
+  SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && C <= 2048 && dz && (zmask || mask_bits) && ya && yb && mean_a && invstd_a &&
                    mean_b && invstd_b && dy_a && dy_b && partial && coef,
                SSIP_ERR_ARG, "ssip_bn_bwd_dual: bad arguments");
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_bwd_dual: unsupported size");
@@ -447,11 +469,12 @@ int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zm
   f.coef[0] = coef; f.coef[1] = coef + 3 * C;
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_dual_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
-                       (const T*)zmask, (const T*)ya, (const T*)yb, mean_a, invstd_a, mean_b, invstd_b, pa, pb);
+                       (const T*)zmask, mask_bits, (const T*)ya, (const T*)yb, mean_a, invstd_a, mean_b, invstd_b, pa,
+                       pb);
     hipLaunchKernelGGL(bn_bwd_finalize_dual_kernel, dim3(2 * C), dim3(1024), 0, st, C, blocks, (long)M, f,
                        accumulate);
     hipLaunchKernelGGL(bn_bwd_apply_dual_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
-                       (const T*)dz, (const T*)zmask, (const T*)ya, (const T*)yb, coef, coef + 3 * C, (T*)dy_a,
+                       (const T*)dz, (const T*)zmask, mask_bits, (const T*)ya, (const T*)yb, coef, coef + 3 * C, (T*)dy_a,
                        (T*)dy_b);
   });
   return ::ssip::check_launch("bn_bwd_dual");
@@ -463,7 +486,8 @@ int64_t ssip_bn_bwd_partial_floats(int64_t M, int C) {
   return ((M + rows - 1) / rows) * (int64_t)C * 2;
 }
 
-static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* zmask, const float* mscale,
+static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mbits,
+                       const float* mscale,
                        const float* mshift, const void* y, const float* mean, const float* invstd,
                        const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy, void* dpre,
                        float* partial, float* coef, void* stream) {
@@ -476,11 +500,11 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
-                       (const T*)zmask, (const T*)y, mean, invstd, mscale, mshift, partial);
+                       (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, (long)M, 1, partial, gamma, mean,
                        invstd, dgamma, dbeta, accumulate, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
-                       (const T*)zmask, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
+                       (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
 }
@@ -498,16 +522,19 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                      invstd, dgamma, dbeta, accumulate, coef);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
-                       (const T*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr, (const float*)nullptr,
+                       (const T*)nullptr, (const uint8_t*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr,
+                       (const float*)nullptr,
                        (const float*)nullptr);
   });
   return ::ssip::check_launch("bn_bwd_from_partials");
 }
 
-int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const void* y, const float* mean,
+int ssip_bn_bwd(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mask_bits,
+                const void* y, const float* mean,
                 const float* invstd, const float* gamma, float* dgamma, float* dbeta, int accumulate, void* dy,
                 void* dpre, float* partial, float* coef, void* stream) {
-  return bn_bwd_impl(dtype, M, C, dz, zmask, nullptr, nullptr, y, mean, invstd, gamma, dgamma, dbeta, accumulate, dy,
+  return bn_bwd_impl(dtype, M, C, dz, zmask, mask_bits, nullptr, nullptr, y, mean, invstd, gamma, dgamma, dbeta,
+                     accumulate, dy,
                      dpre, partial, coef, stream);
 }
 
@@ -515,7 +542,8 @@ int ssip_bn_relu_bwd(int dtype, int64_t M, int C, const void* dz, const void* y,
                      const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
                      float* dbeta, int accumulate, void* dy, float* partial, float* coef, void* stream) {
   SSIP_REQUIRE(scale && shift, SSIP_ERR_ARG, "ssip_bn_relu_bwd: scale/shift required");
-  return bn_bwd_impl(dtype, M, C, dz, nullptr, scale, shift, y, mean, invstd, gamma, dgamma, dbeta, accumulate, dy,
+  return bn_bwd_impl(dtype, M, C, dz, nullptr, nullptr, scale, shift, y, mean, invstd, gamma, dgamma, dbeta,
+                     accumulate, dy,
                      nullptr, partial, coef, stream);
 }
 

@@ -77,7 +77,8 @@ static inline int bn_bwd_finalize_grid(int C) { return C; }
 // Block: 256 threads; each thread owns an 8-channel chunk; threads/row = C/8.
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int rows_per_block, const T* __restrict__ dz,
-                                     const T* __restrict__ zmask, const T* __restrict__ y,
+                                     const T* __restrict__ zmask, const uint8_t* __restrict__ mbits,
+                                     const T* __restrict__ y,
                                      const float* __restrict__ mean, const float* __restrict__ invstd,
                                      const float* __restrict__ mscale, const float* __restrict__ mshift,
                                      float* __restrict__ partial) {
@@ -99,12 +100,13 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
     load_f8(msc, mscale + c0);
     load_f8(msh, mshift + c0);
   }
-  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, const Vec8<T>& yy) {
+  auto acc = [&](const Vec8<T>& g, const Vec8<T>& zz, uint32_t mb, const Vec8<T>& yy) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float d = g.get(j);
       if (zmask) d = zz.get(j) > 0.f ? d : 0.f;
       if (amask) d = __builtin_fmaf(yy.get(j), msc[j], msh[j]) > 0.f ? d : 0.f;
+      d = ((mb >> j) & 1u) ? d : 0.f;
       const float xh = (yy.get(j) - mu[j]) * is[j];
       sd[j] += d;
       sx[j] += d * xh;
@@ -116,6 +118,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
     long r = r0 + rsub;
     for (; r + rpi < r1; r += 2 * rpi) {
       Vec8<T> g0, g1, z0, z1, y0, y1;
+      uint32_t m0 = 0xFFu, m1 = 0xFFu;
       g0.load(dz + r * C + c0);
       g1.load(dz + (r + rpi) * C + c0);
       y0.load(y + r * C + c0);
@@ -124,15 +127,21 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
         z0.load(zmask + r * C + c0);
         z1.load(zmask + (r + rpi) * C + c0);
       }
-      acc(g0, z0, y0);
-      acc(g1, z1, y1);
+      if (mbits) {
+        m0 = mbits[r * cpr + chunk];
+        m1 = mbits[(r + rpi) * cpr + chunk];
+      }
+      acc(g0, z0, m0, y0);
+      acc(g1, z1, m1, y1);
     }
     if (r < r1) {
       Vec8<T> g0, z0, y0;
+      uint32_t m0 = 0xFFu;
       g0.load(dz + r * C + c0);
       y0.load(y + r * C + c0);
       if (zmask) z0.load(zmask + r * C + c0);
-      acc(g0, z0, y0);
+      if (mbits) m0 = mbits[r * cpr + chunk];
+      acc(g0, z0, m0, y0);
     }
   }
   __shared__ float red[2][256][9];

@@ -347,7 +347,8 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   SSIP_DISPATCH_DTYPE(dtype, T, {
     if (ymax)
       hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(red_blocks), dim3(256), 0, st, Mp, C, prow, (const T*)dpool,
-                         (const T*)nullptr, (const T*)ymax, mean, invstd, scale, shift, partial);
+                         (const T*)nullptr, (const uint8_t*)nullptr, (const T*)ymax, mean, invstd, scale, shift,
+                         partial);
     else
       hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                          pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);

@@ -333,15 +333,16 @@ def bn_eval_coeffs(C: int, gamma, beta, running_mean, running_var, eps: float, m
          _p(invstd), _p(scale), _p(shift), stream_ptr())
 
 
-def bn_apply(M: int, C: int, y, scale, shift, residual, relu: bool, z) -> None:
+def bn_apply(M: int, C: int, y, scale, shift, residual, relu: bool, z, mbits=None) -> None:
+    """mbits: uint8 [M*C/8] receives the ReLU mask (bit j of byte i = z[8i+j] > 0)."""
     call("ssip_bn_apply", dtype_code(y), M, C, _p(y), _p(scale), _p(shift), _p(residual), int(relu), _p(z),
-         stream_ptr())
+         _p(mbits), stream_ptr())
 
 
-def bn_apply2(M: int, C: int, y, scale, shift, y2, scale2, shift2, relu: bool, z) -> None:
+def bn_apply2(M: int, C: int, y, scale, shift, y2, scale2, shift2, relu: bool, z, mbits=None) -> None:
     """z = relu(y*scale + shift + y2*scale2 + shift2) (block output with a downsample BN residual)."""
     call("ssip_bn_apply2", dtype_code(y), M, C, _p(y), _p(scale), _p(shift), _p(y2), _p(scale2), _p(shift2),
-         int(relu), _p(z), stream_ptr())
+         int(relu), _p(z), _p(mbits), stream_ptr())
 
 
 def bn_bwd_dual_partial_floats(M: int, C: int) -> int:
@@ -352,9 +353,10 @@ def bn_bwd_dual_partial_floats(M: int, C: int) -> int:
 
 
 def bn_bwd_dual(M: int, C: int, dz, zmask, ya, mean_a, invstd_a, gamma_a, dgamma_a, dbeta_a, yb, mean_b, invstd_b,
-                gamma_b, dgamma_b, dbeta_b, accumulate: bool, dy_a, dy_b, partial, coef) -> None:
-    """Backward of z = relu(BN_a(ya) + BN_b(yb)) (ssip_bn_bwd_dual); coef: 6*C floats."""
-    call("ssip_bn_bwd_dual", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(ya), _p(mean_a), _p(invstd_a), _p(gamma_a),
+                gamma_b, dgamma_b, dbeta_b, accumulate: bool, dy_a, dy_b, partial, coef, mbits=None) -> None:
+    """Backward of z = relu(BN_a(ya) + BN_b(yb)) (ssip_bn_bwd_dual); coef: 6*C floats.
+    The ReLU mask comes from zmask (z > 0) or, when zmask is None, from mbits."""
+    call("ssip_bn_bwd_dual", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(mbits), _p(ya), _p(mean_a), _p(invstd_a), _p(gamma_a),
          _p(dgamma_a), _p(dbeta_a), _p(yb), _p(mean_b), _p(invstd_b), _p(gamma_b), _p(dgamma_b), _p(dbeta_b),
          int(accumulate), _p(dy_a), _p(dy_b), _p(partial), _p(coef), stream_ptr())
 
@@ -364,8 +366,9 @@ def bn_bwd_partial_floats(M: int, C: int) -> int:
 
 
 def bn_bwd(M: int, C: int, dz, zmask, y, mean, invstd, gamma, dgamma, dbeta, accumulate: bool, dy, dpre, partial,
-           coef) -> None:
-    call("ssip_bn_bwd", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(y), _p(mean), _p(invstd), _p(gamma),
+           coef, mbits=None) -> None:
+    """ReLU mask from zmask (z > 0) or, when zmask is None, from mbits (ssip_bn_apply's mask bits)."""
+    call("ssip_bn_bwd", dtype_code(dz), M, C, _p(dz), _p(zmask), _p(mbits), _p(y), _p(mean), _p(invstd), _p(gamma),
          _p(dgamma), _p(dbeta), int(accumulate), _p(dy), _p(dpre), _p(partial), _p(coef), stream_ptr())
 
 

@@ -149,6 +149,7 @@ class _ConvRec:
     y: torch.Tensor          # conv output [N,P,Q,K] (pre-BN)
     stats: torch.Tensor      # [4, K] mean, invstd, scale, shift
     z: Optional[torch.Tensor] = None   # post BN(+add)+ReLU output (mask source)
+    zbits: Optional[torch.Tensor] = None  # its ReLU mask, one bit per element (the backward reads this, not z)
 
 
 @dataclass
@@ -409,15 +410,18 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
         last = recs[-1]
         ds = None
         out = torch.empty_like(last.y)
+        # the backward masks with 1 bit per element instead of re-reading out
+        bits = torch.empty(out.numel() // 8, device=dev, dtype=torch.uint8) if save else None
         if blk.downsample is not None:
             # out = relu(bn2(y2) + bn_ds(y_ds)): the downsample's BN is formed in
             # registers by the same pass (its output is never stored)
             ds = _conv_bn(model, blk.downsample[0], blk.downsample[1], x, N, Hc, Wc, train, save, upd)
             ops.bn_apply2(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], ds.y, ds.stats[2],
-                          ds.stats[3], True, out)
+                          ds.stats[3], True, out, bits)
         else:
-            ops.bn_apply(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], x, True, out)
+            ops.bn_apply(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], x, True, out, bits)
         last.z = out
+        last.zbits = bits
         if save:
             sv.blocks.append((recs, ds, x))
         x, Hc, Wc = out, h, w
@@ -584,15 +588,16 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             acc = acc2
         return dgam, dbet, acc
 
-    def bn_backward(rec: _ConvRec, dzin, zmask, dpre=None):
-        """BN(+ReLU) backward with its own reduction pass."""
+    def bn_backward(rec: _ConvRec, dzin, zmask, dpre=None, mbits=None):
+        """BN(+ReLU) backward with its own reduction pass; the ReLU mask from
+        zmask (z > 0) or from the forward's mask bits."""
         g = rec.geom
         M = N * g.P * g.Q
         dgam, dbet, acc = bn_grads(rec)
         dy = torch.empty_like(rec.y)
         partial = torch.empty(ops.bn_bwd_partial_floats(M, g.K), device=dev, dtype=torch.float32)
         ops.bn_bwd(M, g.K, dzin, zmask, rec.y, rec.stats[0], rec.stats[1], rec.bn.weight.detach(), dgam, dbet, acc,
-                   dy, dpre, partial, coef_buf[: 3 * g.K])
+                   dy, dpre, partial, coef_buf[: 3 * g.K], mbits)
         return dy
 
     def bn_relu_backward(rec: _ConvRec, dzin):
@@ -618,7 +623,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                                  rec.bn.weight.detach(), dgam, dbet, acc, dy, coef_buf[: 3 * g.K])
         return dy
 
-    def bn_backward_dual(rec_a: _ConvRec, rec_b: _ConvRec, dzin, zmask):
+    def bn_backward_dual(rec_a: _ConvRec, rec_b: _ConvRec, dzin, zmask, mbits=None):
         """Backward of z = relu(BN_a(y_a) + BN_b(y_b)) in one reduction and one
         apply pass (the masked gradient that feeds both is never stored);
         None when the two BNs' gradients do not both accumulate or both start fresh."""
@@ -634,7 +639,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         partial = torch.empty(ops.bn_bwd_dual_partial_floats(M, g.K), device=dev, dtype=torch.float32)
         ops.bn_bwd_dual(M, g.K, dzin, zmask, rec_a.y, rec_a.stats[0], rec_a.stats[1], rec_a.bn.weight.detach(), ga,
                         ba, rec_b.y, rec_b.stats[0], rec_b.stats[1], rec_b.bn.weight.detach(), gb, bb, acc, dya, dyb,
-                        partial, coef_buf[: 6 * g.K])
+                        partial, coef_buf[: 6 * g.K], mbits)
         return dya, dyb
 
     def conv_wgrad(rec: _ConvRec, dy):
@@ -677,15 +682,16 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         below = sv.blocks[bi - 1][0][-1] if bi > 0 else None  # BN+ReLU producing this block's input
         last = recs[-1]
         dual = None
+        zm, zb = (None, last.zbits) if last.zbits is not None else (last.z, None)
         if pending is None and ds is not None:
-            dual = bn_backward_dual(last, ds, dz, last.z)
+            dual = bn_backward_dual(last, ds, dz, zm, zb)
         dpre = None
         if dual is not None:
             dy, dy_ds = dual
         else:
             if pending is None:
                 dpre = torch.empty_like(last.y)
-                dy = bn_backward(last, dz, last.z, dpre)
+                dy = bn_backward(last, dz, zm, dpre, zb)
             else:
                 dpre, part, tiles = pending
                 dy = bn_backward_fused(last, dpre, part, tiles)

@@ -149,3 +149,46 @@ def test_bn_bwd_dual(dev, dtname):
                     part, coef)
     torch.cuda.synchronize()
     assert rel(dgb, 2 * gbd.grad) < tol and rel(dba, 2 * bad_.grad) < tol
+
+
+@pytest.mark.parametrize("dtname", ["f32", "bf16"])
+def test_relu_mask_bits(dev, dtname):
+    """ssip_bn_apply(2)'s mask bits (bit j of byte i = z[8i+j] > 0) and the
+    backward passes that read them instead of z: the same outputs, bit for bit."""
+    dt = DT if dtname == "bf16" else torch.float32
+    torch.manual_seed(3)
+    M, C = 2 * 7 * 7 + 3, 64
+    y, y2, r = (torch.randn(M, C, device=dev).to(dt) for _ in range(3))
+    sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3
+    sc2, sh2 = torch.randn(C, device=dev), torch.randn(C, device=dev) * 0.3
+    z, bits = torch.empty_like(y), torch.empty(M * C // 8, device=dev, dtype=torch.uint8)
+    ops.bn_apply(M, C, y, sc, sh, r, True, z, bits)
+    z2, bits2 = torch.empty_like(y), torch.empty_like(bits)
+    ops.bn_apply2(M, C, y, sc, sh, y2, sc2, sh2, True, z2, bits2)
+    torch.cuda.synchronize()
+    w = (2 ** torch.arange(8, device=dev)).to(torch.int32)
+    for zz, bb in ((z, bits), (z2, bits2)):
+        want = ((zz.float() > 0).reshape(-1, 8).to(torch.int32) * w).sum(1).to(torch.uint8)
+        assert torch.equal(bb, want)
+    dz = torch.randn(M, C, device=dev).to(dt)
+    mean, invstd = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    gamma = torch.rand(C, device=dev) + 0.5
+    outs = []
+    for zm, mb in ((z, None), (None, bits)):
+        dg, db, dy, dpre = torch.empty(C, device=dev), torch.empty(C, device=dev), torch.empty_like(y), torch.empty_like(y)
+        part = torch.empty(ops.bn_bwd_partial_floats(M, C), device=dev)
+        coef = torch.empty(3 * C, device=dev)
+        ops.bn_bwd(M, C, dz, zm, y, mean, invstd, gamma, dg, db, False, dy, dpre, part, coef, mbits=mb)
+        outs.append((dg, db, dy, dpre))
+    for zm, mb in ((z2, None), (None, bits2)):
+        t = [torch.empty(C, device=dev) for _ in range(4)]
+        dya, dyb = torch.empty_like(y), torch.empty_like(y)
+        part = torch.empty(ops.bn_bwd_dual_partial_floats(M, C), device=dev)
+        coef = torch.empty(6 * C, device=dev)
+        ops.bn_bwd_dual(M, C, dz, zm, y, mean, invstd, gamma, t[0], t[1], y2, mean, invstd, gamma, t[2], t[3], False,
+                        dya, dyb, part, coef, mbits=mb)
+        outs.append(tuple(t) + (dya, dyb))
+    torch.cuda.synchronize()
+    for a, b in ((outs[0], outs[1]), (outs[2], outs[3])):
+        for x, y_ in zip(a, b):
+            assert torch.equal(x, y_)

@@ -2415,6 +2415,7 @@ static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
 }
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st);
+static int device_cus();
 
 // Default LDS-DMA configuration for a bf16 GEMM view (M x Ng, reduction Kg).
 // Chosen from tools/tune_conv.py over the ResNet-18 train-step shapes
@@ -2504,16 +2505,32 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   if (mode == MODE_WGRAD) {
     const int tiles = ceil_div(a.M, pl.bm) * ceil_div(a.Ng, pl.bn);
     const int total_ks = ceil_div(a.Mred, BK);
-    // ~1024 blocks (4 per CU), slab <= 64 MiB (stays in the Infinity Cache),
-    // >= 16 k-steps per split (keeps the slab and its reduction small)
-    int target = 1024;
-    if (const char* e = getenv("SSIP_WGRAD_BLOCKS")) target = std::max(1, atoi(e));  // tuning override
-    int splits = ceil_div(target, tiles);
+    // split count: every split is one more fp32 slab written here and read by
+    // the reduce; the grid should end on a full wave of resident workgroups
+    // (a launch of 540 workgroups on 512 slots runs two waves for 5 % more
+    // work).  Cost in k-step times: waves * k-steps per split + the slab
+    // round trip (~0.27 k-step per MiB, tools/tune_wgrad_splits.py);
+    // slab <= 64 MiB, >= 16 k-steps per split.
     const long slab_split = (long)a.M * a.Ng * 4;
     const int cap_bytes = (int)std::max<long>(1, (64l << 20) / slab_split);
-    if (splits > cap_bytes) splits = cap_bytes;
-    const int max_splits = std::max(1, total_ks / 16);
-    if (splits > max_splits) splits = max_splits;
+    const int max_splits = std::max(1, std::min(cap_bytes, total_ks / 16));
+    int splits = 1;
+    if (const char* e = getenv("SSIP_WGRAD_BLOCKS")) {  // tuning override: target workgroup count
+      splits = std::min(max_splits, ceil_div(std::max(1, atoi(e)), tiles));
+    } else if (pl.stages > 0) {
+      const int nt = 64 * pl.wmw * pl.wnw;
+      const int lds = 2 * 64 * (pl.bm + pl.bn) * 2;
+      const int per_cu = std::max(1, std::min(2048 / nt, 163840 / lds));
+      const long slots = (long)device_cus() * per_cu;
+      double best = 1e30;
+      for (int s = 1; s <= max_splits; ++s) {
+        const long waves = ((long)tiles * s + slots - 1) / slots;
+        const double cost = (double)waves * ceil_div(total_ks, s) + 0.27 * s * (double)slab_split / (1 << 20);
+        if (cost < best - 1e-9) { best = cost; splits = s; }
+      }
+    } else {
+      splits = std::min(max_splits, ceil_div(1024, tiles));
+    }
     if (splits < 1) splits = 1;
     a.ksteps = ceil_div(total_ks, splits);
     splits = ceil_div(total_ks, a.ksteps);

@@ -11,7 +11,7 @@ from tune_conv import shapes, time_fn  # noqa: E402
 dev = torch.device("cuda:0")
 bf = torch.bfloat16
 ws = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
-targets = [256, 512, 768, 1024, 1536, 2048]
+targets = ["model", 512, 1024, "model2"]  # "model": the planner's own choice (SSIP_WGRAD_BLOCKS unset)
 tot = {t: 0.0 for t in targets}
 for nm, g in shapes(256):
     x = torch.randn(g.N, g.H, g.W, g.C, device=dev).to(bf)
@@ -19,8 +19,11 @@ for nm, g in shapes(256):
     dw = torch.empty(g.K, g.C, g.R, g.S, device=dev)
     line = f"{nm:9s}"
     for t in targets:
-        os.environ["SSIP_WGRAD_BLOCKS"] = str(t)
-        us = time_fn(lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), 10)
+        if str(t).startswith("model"):
+            os.environ.pop("SSIP_WGRAD_BLOCKS", None)
+        else:
+            os.environ["SSIP_WGRAD_BLOCKS"] = str(t)
+        us = time_fn(lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), 20)
         tot[t] += us
         line += f"  {t}:{us:6.1f}"
     print(line, flush=True)

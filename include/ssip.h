@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 6
+#define SSIP_ABI_VERSION 7
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -99,6 +99,12 @@ int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype);
 int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
                        const void* zmask, const void* y, const float* mean, const float* invstd, void* dpre,
                        float* partial, void* stream);
+/* Eval-mode conv + folded BatchNorm (+ residual) (+ ReLU), one launch:
+ *   y = act(conv(x, w') + bias[k] (+ residual)),  w' = w * scale[k] (ssip_wprep.kscale)
+ * (torchvision BasicBlock / Bottleneck in eval mode: bn(conv(x)) with running
+ * statistics is an affine map per output channel).  Not for the C == 4 stem. */
+int ssip_conv_fwd_bias(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, const float* bias,
+                       const void* residual, int relu, void* y, void* stream);
 int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d);
 /* dw_kcrs (fp32, torchvision layout [K][c_real][R][s_real]) (+)= dW */
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
@@ -264,13 +270,17 @@ int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, f
 int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, const float* w_kcrs, void* w_krsc,
                      void* w_crsk, void* stream);
 /* Batched form: every stale conv weight of a model in one launch (per step).
- * krsc or crsk may be NULL per item; count <= SSIP_WPREP_MAX per call. */
+ * krsc or crsk may be NULL per item; count <= SSIP_WPREP_MAX per call.
+ * kscale (nullable): per-output-channel factor applied before the conversion,
+ * w'[k] = w[k] * kscale[k] -- an eval-mode BatchNorm folded into the conv
+ * (bias = its shift, ssip_bn_eval_coeffs). */
 #define SSIP_WPREP_MAX 32
 typedef struct ssip_wprep {
   int K, C, R, S, Cp, Sp;
   const float* w_kcrs;
   void* w_krsc;
   void* w_crsk;
+  const float* kscale;
 } ssip_wprep;
 int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* items, void* stream);
 

@@ -70,8 +70,10 @@ struct ConvArgs {
   const void* A;
   const void* B;
   void* out;
-  const void* add;
+  const void* add;     // DGRAD: residual-gradient add; FWD: residual (ssip_conv_fwd_bias)
   float* partial;
+  const float* bias;   // FWD: per-output-channel bias (a folded eval-mode BatchNorm), nullable
+  int relu;            // FWD: ReLU on the output (after bias and residual)
   // DGRAD post-op (BN backward of the layer that produced this conv's input):
   // out = (dgrad + add) * (pmask > 0); per-(tile, channel) sums of out and
   // out * (py - pmean) * pinvstd into partial [tiles_m][Ng][2].
@@ -401,6 +403,12 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
   // stage the tile through LDS (main loop finished: the staging buffers are free)
   constexpr int EROW = BN * (int)sizeof(T) + 16;  // padded row (bytes)
   {
+    float bcol[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + cbase + j * 16;
+      bcol[j] = (MODE == MODE_FWD && a.bias != nullptr && n < a.Ng) ? a.bias[n] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -409,7 +417,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
         for (int e = 0; e < 4; ++e) {
           const int row = rbase + i * 16 + e;
           const int col = cbase + j * 16;
-          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) = from_f32<T>(acc[i][j][e]);
+          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) = from_f32<T>(acc[i][j][e] + bcol[j]);
         }
   }
   __syncthreads();
@@ -450,6 +458,19 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
           r.load(Add + orow * a.Ng + n);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v.set(j, v.get(j) + r.get(j));
+        }
+      }
+      if constexpr (MODE == MODE_FWD) {  // folded eval BN: + residual, ReLU (bias already in)
+        if (Add || a.relu) {
+          Vec8<T> r;
+          if (Add) r.load(Add + orow * a.Ng + n);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = v.get(j);
+            if (Add) t += r.get(j);
+            if (a.relu) t = t > 0.f ? t : 0.f;
+            v.set(j, t);
+          }
         }
       }
       v.store(Out + orow * a.Ng + n);
@@ -1492,8 +1513,10 @@ struct HaloArgs {
   const __bf16* X;    // [N][H][W][64]   (FWD: x, DGRAD: dy)
   const __bf16* Wt;   // [Ncols][9][64]  (FWD: w_krsc, DGRAD: w_crsk)
   __bf16* out;        // [N][H][W][Ncols]
-  const __bf16* add;  // DGRAD residual gradient (nullable, may alias out)
+  const __bf16* add;  // DGRAD residual gradient / FWD residual (nullable, may alias out)
   float* partial;     // FWD BN records (nullable)
+  const float* bias;  // FWD per-channel bias (folded eval BN), nullable
+  int relu;           // FWD ReLU after bias and residual
   uint32_t x_bytes, w_bytes, o_bytes;
   int N, H, W, Ncols, TR, tiles, units, flip;
   int dbg;  // ablation (tools/time_halo.py): 1 = no MFMA, 2 = no epilogue
@@ -1707,6 +1730,10 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) off[i][e] = obase + rowoff[i][e];
+      float bcol[FN];  // folded eval BN (FWD): per-column bias
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) bcol[jj] = a.bias ? a.bias[jn * BN + cbase + jj * 16] : 0.f;
+      const float lo = a.relu ? 0.f : -__builtin_huge_valf();
       if (a.add) {
         short r[FM][FN][4];
 #pragma unroll
@@ -1722,7 +1749,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
           for (int jj = 0; jj < FN; ++jj)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const T o = from_f32<T>(to_f32(from_f32<T>(acc[i][jj][e])) + to_f32(__builtin_bit_cast(T, r[i][jj][e])));
+              const float t = to_f32(from_f32<T>(acc[i][jj][e] + bcol[jj])) + to_f32(__builtin_bit_cast(T, r[i][jj][e]));
+              const T o = from_f32<T>(fmaxf(t, lo));
               __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off[i][e] + jj * 32, 0, 0);
             }
       } else {
@@ -1732,8 +1760,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
           for (int jj = 0; jj < FN; ++jj)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(acc[i][jj][e])), rsO,
-                                                    off[i][e] + jj * 32, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b16(
+                  __builtin_bit_cast(short, from_f32<T>(fmaxf(acc[i][jj][e] + bcol[jj], lo))), rsO,
+                  off[i][e] + jj * 32, 0, 0);
       }
     }
     if (more && !prefetch) {
@@ -2854,8 +2883,11 @@ static bool stem_wg_plan(const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
 }
 
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
-                       void* out, const void* add, float* partial, hipStream_t st) {
+                       void* out, const void* add, float* partial, hipStream_t st, const float* bias = nullptr,
+                       int relu = 0) {
   HaloArgs h;
+  h.bias = bias;
+  h.relu = relu;
   h.X = static_cast<const __bf16*>(X);
   h.Wt = static_cast<const __bf16*>(Wt);
   h.out = static_cast<__bf16*>(out);
@@ -2932,6 +2964,24 @@ int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
   if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
   if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
   return ceil_div(pl.args.M, pl.bm);
+}
+
+int ssip_conv_fwd_bias(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, const float* bias,
+                       const void* residual, int relu, void* y, void* stream) {
+  Plan pl;
+  int rc = plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl);
+  if (rc) return rc;
+  SSIP_REQUIRE(!pl.conv1, SSIP_ERR_ARG, "ssip_conv_fwd_bias: not for the C = 4 stem");
+  SSIP_REQUIRE(x && w_krsc && bias && y, SSIP_ERR_ARG, "ssip_conv_fwd_bias: null pointer");
+  if (pl.stages > 0 && d->R * d->S > 32) fallback_regstaged(pl);
+  HaloPlan hp;
+  if (halo_plan(MODE_FWD, d, dtype, hp))
+    return launch_halo(MODE_FWD, d, hp, x, w_krsc, y, residual, nullptr, (hipStream_t)stream, bias, relu ? 1 : 0);
+  pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = nullptr;
+  pl.args.add = residual; pl.args.bias = bias; pl.args.relu = relu ? 1 : 0;
+  pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
+  pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
+  SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_FWD, T>(pl, (hipStream_t)stream));
 }
 
 int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, void* dx,

@@ -114,7 +114,10 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(const WprepTable
   for (int kk = ty; kk < 64; kk += 4) {
     const int k = k0 + kk, c = c0 + tx;
     float v = 0.f;
-    if (k < e.K && c < e.C && s < e.S) v = e.w_kcrs[(((long)k * e.C + c) * e.R + r) * e.S + s];
+    if (k < e.K && c < e.C && s < e.S) {
+      v = e.w_kcrs[(((long)k * e.C + c) * e.R + r) * e.S + s];
+      if (e.kscale) v *= e.kscale[k];
+    }
     tile[kk][tx] = v;
   }
   __syncthreads();

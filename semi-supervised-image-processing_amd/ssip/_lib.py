@@ -29,7 +29,7 @@ def abi_version_expected() -> int:
     return int(m.group(1)) if m else ABI_VERSION
 
 
-ABI_VERSION = 6  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
+ABI_VERSION = 7  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1
@@ -49,7 +49,8 @@ WPREP_MAX = 32
 
 class WPrep(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("K", "C", "R", "S", "Cp", "Sp")] + [
-        ("w_kcrs", ctypes.c_void_p), ("w_krsc", ctypes.c_void_p), ("w_crsk", ctypes.c_void_p)]
+        ("w_kcrs", ctypes.c_void_p), ("w_krsc", ctypes.c_void_p), ("w_crsk", ctypes.c_void_p),
+        ("kscale", ctypes.c_void_p)]
 
 
 class AugParam(ctypes.Structure):
@@ -84,6 +85,7 @@ _SIGS = {
     "ssip_conv_fwd": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad_ds": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_conv_fwd_bias": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "ssip_conv_dgrad_bn_partial_floats": (_c_i64, [_PD]),
     "ssip_conv_dgrad_bn_partial_tiles": (_c_int, [_PD, _c_int]),
     "ssip_conv_dgrad_bn": (_c_int, [_PD, _c_int] + [_vp] * 10),

@@ -196,6 +196,18 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor
     call("ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial), stream_ptr())
 
 
+def conv_fwd_bias(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, bias: torch.Tensor,
+                  residual: Optional[torch.Tensor], relu: bool, y: torch.Tensor) -> None:
+    """y = act(conv(x, w) + bias (+ residual)): eval-mode conv with its BN folded in (ssip_conv_fwd_bias)."""
+    assert x.numel() == g.N * g.H * g.W * g.C, "conv_fwd_bias: x shape"
+    assert w_krsc.numel() == g.K * g.R * g.S * g.C, "conv_fwd_bias: w shape"
+    assert y.numel() == g.N * g.P * g.Q * g.K and bias.numel() == g.K, "conv_fwd_bias: y / bias shape"
+    if residual is not None:
+        assert residual.numel() == y.numel() and residual.dtype == y.dtype
+    call("ssip_conv_fwd_bias", g.desc(), dtype_code(x), _p(x), _p(w_krsc), _p(bias), _p(residual), int(relu), _p(y),
+         stream_ptr())
+
+
 def conv_dgrad(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx: torch.Tensor,
                dx_add: Optional[torch.Tensor] = None) -> None:
     assert dy.numel() == g.N * g.P * g.Q * g.K, "conv_dgrad: dy shape"
@@ -298,18 +310,23 @@ def stem_bwd_wgrad(g: ConvGeom, dpool, idx, y, x, scale, shift, coef, dw, accumu
 
 
 def weight_prep_batch(items, dtype: torch.dtype) -> None:
-    """items: [(w_kcrs fp32, Cp, Sp, krsc or None, crsk or None)] -> one launch per 32."""
+    """items: [(w_kcrs fp32, Cp, Sp, krsc or None, crsk or None[, kscale fp32 [K] or None])]
+    -> one launch per 32 (kscale: per-output-channel factor, a folded eval BN)."""
     for i in range(0, len(items), _lib.WPREP_MAX):
         chunk = items[i:i + _lib.WPREP_MAX]
         arr = (_lib.WPrep * len(chunk))()
-        for j, (w, Cp, Sp, krsc, crsk) in enumerate(chunk):
+        for j, item in enumerate(chunk):
+            w, Cp, Sp, krsc, crsk = item[:5]
+            ksc = item[5] if len(item) > 5 else None
             assert w.dtype == torch.float32 and w.is_contiguous()
             K, C, R, S = w.shape
             if krsc is not None:
                 assert krsc.dtype == dtype and krsc.numel() == K * R * Sp * Cp
             if crsk is not None:
                 assert crsk.dtype == dtype and crsk.numel() == K * R * Sp * Cp
-            arr[j] = _lib.WPrep(K, C, R, S, Cp, Sp, _p(w), _p(krsc), _p(crsk))
+            if ksc is not None:
+                assert ksc.dtype == torch.float32 and ksc.numel() == K
+            arr[j] = _lib.WPrep(K, C, R, S, Cp, Sp, _p(w), _p(krsc), _p(crsk), _p(ksc))
         call("ssip_weight_prep_batch", _DT[dtype], len(chunk), arr, stream_ptr())
 
 

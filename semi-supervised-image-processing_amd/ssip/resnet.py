@@ -199,6 +199,9 @@ class SSIPResNet(nn.Module):
         self.bn_update_running = True   # may be switched off for no-update batch-stat passes
         # (id(conv), dtype) -> [krsc, crsk or None, weight version they were made from]
         self._prep: Dict[Tuple[int, torch.dtype], list] = {}
+        # (id(conv), dtype) -> [krsc with the eval BN folded in, bias, state stamp]
+        self._fold: Dict[Tuple[int, torch.dtype], list] = {}
+        self._bn_epoch = 0
         self._arena = None
         self.embedding_only = False
 
@@ -219,6 +222,7 @@ class SSIPResNet(nn.Module):
     def set_compute_dtype(self, dtype: str) -> "SSIPResNet":
         self.compute_dtype = _DTYPES[dtype]
         self._prep.clear()
+        self._fold.clear()
         return self
 
     def blocks(self):
@@ -228,6 +232,7 @@ class SSIPResNet(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):
         self._prep.clear()
+        self._fold.clear()
         self._arena = None
         return super()._apply(fn, *args, **kwargs)
 
@@ -393,7 +398,29 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
         sv.stem, sv.pool_out, sv.pool_idx, sv.pool_hw = rec, pool, idx, (g.P, g.Q)
         sv.pool_ymax = ymax
     x, Hc, Wc = pool, Hp, Wp
+    fold = not train and _FOLD_EVAL_BN
+    if fold:
+        _prepare_folded(model)
     for blk in model.blocks():
+        if fold:
+            # eval mode: each conv carries its BN as scaled weights + bias, and the
+            # ReLU / residual add run in the conv epilogue (no BN passes)
+            ident = x
+            if blk.downsample is not None:
+                gd = _geom(blk.downsample[0], N, Hc, Wc)
+                kr, b = model._fold[(id(blk.downsample[0]), dt)][:2]
+                ident = torch.empty((N, gd.P, gd.Q, gd.K), device=dev, dtype=dt)
+                ops.conv_fwd_bias(gd, x, kr, b, None, False, ident)
+            z, h, w = x, Hc, Wc
+            stages = blk.stages()
+            for i, (conv, bn) in enumerate(stages):
+                g = _geom(conv, N, h, w)
+                kr, b = model._fold[(id(conv), dt)][:2]
+                out = torch.empty((N, g.P, g.Q, g.K), device=dev, dtype=dt)
+                ops.conv_fwd_bias(g, z, kr, b, ident if i == len(stages) - 1 else None, True, out)
+                z, h, w = out, g.P, g.Q
+            x, Hc, Wc = z, h, w
+            continue
         recs = []
         z = x
         h, w = Hc, Wc
@@ -439,7 +466,45 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
     sv.last, sv.last_pq = x, Hc * Wc
     if train and upd:
         _bump_batches_tracked(model)
+        model._bn_epoch += 1  # running statistics changed on the device: folded eval weights are stale
     return sv
+
+
+# eval-mode BatchNorm folded into the convs (SSIP_NO_BN_FOLD=1: separate BN passes, for A/B)
+_FOLD_EVAL_BN = os.environ.get("SSIP_NO_BN_FOLD") != "1"
+
+
+def _prepare_folded(model: SSIPResNet) -> None:
+    """Refresh the eval-mode folded copies of every block conv: w' = w * s[k]
+    (s = gamma / sqrt(running_var + eps)) in the compute dtype, bias = beta -
+    running_mean * s.  One coefficient launch per stale BN plus one batched
+    weight launch; reused until a weight, a BN parameter or the running
+    statistics change (torch version counters, and model._bn_epoch for the
+    device-side running-stat updates of a train-mode forward)."""
+    dt = model.compute_dtype
+    items = []
+    for blk in model.blocks():
+        pairs = list(blk.stages()) + ([(blk.downsample[0], blk.downsample[1])] if blk.downsample is not None else [])
+        for conv, bn in pairs:
+            w = conv.weight
+            stamp = (w._version, bn.weight._version, bn.bias._version, bn.running_mean._version,
+                     bn.running_var._version, model._bn_epoch)
+            key = (id(conv), dt)
+            ent = model._fold.get(key)
+            if ent is not None and ent[2] == stamp:
+                continue
+            K, C, R, S = w.shape
+            if ent is None:
+                ent = [torch.empty((K, R, S, C), device=w.device, dtype=dt),
+                       torch.empty(K, device=w.device, dtype=torch.float32), None]
+                model._fold[key] = ent
+            scale = torch.empty(K, device=w.device, dtype=torch.float32)
+            ops.bn_eval_coeffs(K, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.eps,
+                               None, None, scale, ent[1])
+            ent[2] = stamp
+            items.append((w.detach(), C, S, ent[0], None, scale))
+    if items:
+        ops.weight_prep_batch(items, dt)
 
 
 def _bump_batches_tracked(model: SSIPResNet):

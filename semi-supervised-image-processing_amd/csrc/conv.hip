@@ -2454,7 +2454,9 @@ static int device_cus();
 static void choose_glds(int mode, const ConvArgs& a, Plan& pl) {
   pl.stages = 2;
   if (mode == MODE_WGRAD) {
-    if (a.M % 128 == 0) { pl.bm = 128; pl.bn = 128; pl.wmw = 4; pl.wnw = 4; }
+    // 8 waves of 32x64 (profiles/r2_wgrad_tiles.txt: 3-6 % over 16 waves of 32x32,
+    // whose fragment reads load the LDS as much as the MFMAs)
+    if (a.M % 128 == 0) { pl.bm = 128; pl.bn = 128; pl.wmw = 4; pl.wnw = 2; }
     else { pl.bm = 64; pl.bn = 128; pl.wmw = 2; pl.wnw = 4; }
     return;
   }
@@ -2548,7 +2550,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
       splits = std::min(max_splits, ceil_div(std::max(1, atoi(e)), tiles));
     } else if (pl.stages > 0) {
       const int nt = 64 * pl.wmw * pl.wnw;
-      const int lds = 2 * 64 * (pl.bm + pl.bn) * 2;
+      const int lds = std::max(2, pl.stages) * 64 * (pl.bm + pl.bn) * 2;
       const int per_cu = std::max(1, std::min(2048 / nt, 163840 / lds));
       const long slots = (long)device_cus() * per_cu;
       double best = 1e30;

@@ -55,13 +55,20 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/tune.json")
+    ap.add_argument("--modes", default="fdw", help="passes to tune: any of f, d, w")
+    ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--wg", default="", help="wgrad configs 'bm,bn,wm,wn,st;...' (default: the built-in list)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
     ws = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
     part = torch.empty(8 << 20, dtype=torch.float32, device=dev)
     res = []
+    wg_cfgs = [tuple(int(v) for v in c.split(",")) for c in args.wg.split(";") if c] or WG
+    want = set(args.shapes.split(",")) if args.shapes else None
     for nm, g in shapes(args.batch):
+        if want is not None and nm not in want:
+            continue
         x = torch.randn(g.N, g.H, g.W, g.C, device=dev).to(bf)
         w = (torch.randn(g.K, g.R, g.S, g.C, device=dev) * 0.05).to(bf)
         wc = w.permute(3, 1, 2, 0).contiguous()
@@ -72,9 +79,11 @@ def main():
         runs = {
             "f": (FD, lambda: ops.conv_fwd(g, x, w, y, part), y),
             "d": (FD, lambda: ops.conv_dgrad(g, dy, wc, dx), dx),
-            "w": (WG, lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), dw),
+            "w": (wg_cfgs, lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), dw),
         }
         for mode, (cfgs, fn, out) in runs.items():
+            if mode not in args.modes:
+                continue
             os.environ.pop("SSIP_CONV_FORCE", None)
             t_def = time_fn(fn, args.iters)
             ref = out.float().clone()

@@ -272,29 +272,24 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, 
       acc(g0, z0, m0, a0, b0);
     }
   }
-  __shared__ float red[3][256][9];
+  __shared__ float red[256][25];
+  float v[3][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    red[0][threadIdx.x][j] = sd[j];
-    red[1][threadIdx.x][j] = sa[j];
-    red[2][threadIdx.x][j] = sb[j];
+    v[0][j] = sd[j];
+    v[1][j] = sa[j];
+    v[2][j] = sb[j];
   }
-  __syncthreads();
+  chunk_sums<3>(v, cpr, red);
   if (threadIdx.x < cpr) {
     const long o = ((long)c0 * gridDim.x + blockIdx.x) * 2;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float d = 0.f, a = 0.f, b = 0.f;
-      for (int s2 = 0; s2 < rpi; ++s2) {
-        d += red[0][s2 * cpr + threadIdx.x][j];
-        a += red[1][s2 * cpr + threadIdx.x][j];
-        b += red[2][s2 * cpr + threadIdx.x][j];
-      }
       const long oj = o + (long)j * gridDim.x * 2;
-      partial_a[oj] = d;
-      partial_a[oj + 1] = a;
-      partial_b[oj] = d;
-      partial_b[oj + 1] = b;
+      partial_a[oj] = v[0][j];
+      partial_a[oj + 1] = v[1][j];
+      partial_b[oj] = v[0][j];
+      partial_b[oj + 1] = v[2][j];
     }
   }
 }

@@ -73,6 +73,42 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int C, int blocks
 
 static inline int bn_bwd_finalize_grid(int C) { return C; }
 
+// Totals of V per-thread [8]-vectors over the threads that share a channel
+// chunk (tid % cpr, 256-thread block): a butterfly over the lane bits above
+// log2(cpr) inside each wave, then at most 4 groups through LDS in fixed
+// order.  Threads tid < cpr hold the totals on return.  Deterministic (the
+// butterfly leaves identical bits in every lane of a group).
+template <int V>
+__device__ __forceinline__ void chunk_sums(float (&v)[V][8], int cpr, float (*red)[V * 8 + 1]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (cpr < 64) {
+    for (int o = cpr; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += __shfl_xor(v[k][j], o, 64);
+  }
+  const int groups = cpr < 64 ? 4 : 256 / cpr;
+  const bool writer = cpr < 64 ? lane < cpr : true;
+  const int slot = cpr < 64 ? (tid >> 6) * cpr + lane : tid;
+  if (writer)
+#pragma unroll
+    for (int k = 0; k < V; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[slot][k * 8 + j] = v[k][j];
+  __syncthreads();
+  if (tid < cpr) {
+#pragma unroll
+    for (int k = 0; k < V; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = 0.f;
+        for (int g = 0; g < groups; ++g) t += red[g * cpr + tid][k * 8 + j];
+        v[k][j] = t;
+      }
+  }
+}
+
 // per-(row block, channel) sums of dout and dout*xhat.
 // Block: 256 threads; each thread owns an 8-channel chunk; threads/row = C/8.
 template <typename T>
@@ -144,26 +180,21 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
       acc(g0, z0, m0, y0);
     }
   }
-  __shared__ float red[2][256][9];
+  __shared__ float red[256][17];
+  float v[2][8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    red[0][threadIdx.x][j] = sd[j];
-    red[1][threadIdx.x][j] = sx[j];
+    v[0][j] = sd[j];
+    v[1][j] = sx[j];
   }
-  __syncthreads();
-  // threads with rsub == 0 sum over rsub in fixed order
+  chunk_sums<2>(v, cpr, red);
   if (threadIdx.x < cpr) {
     // [C][blocks][2]: each channel's records contiguous for the finalize
     float* out = partial + ((long)c0 * gridDim.x + blockIdx.x) * 2;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float a = 0.f, b = 0.f;
-      for (int s = 0; s < rpi; ++s) {
-        a += red[0][s * cpr + threadIdx.x][j];
-        b += red[1][s * cpr + threadIdx.x][j];
-      }
-      out[(long)j * gridDim.x * 2] = a;
-      out[(long)j * gridDim.x * 2 + 1] = b;
+      out[(long)j * gridDim.x * 2] = v[0][j];
+      out[(long)j * gridDim.x * 2 + 1] = v[1][j];
     }
   }
 }

@@ -372,7 +372,8 @@ struct RowMap {
   }
 };
 
-template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN, bool ALLOW_POST = true>
+template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN, bool ALLOW_POST = true,
+          bool FOLD = false>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
                                                    int n0, int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
                                                    bool pre_loaded, const RowMap& rmap, int split) {
@@ -407,7 +408,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + cbase + j * 16;
-      bcol[j] = (MODE == MODE_FWD && a.bias != nullptr && n < a.Ng) ? a.bias[n] : 0.f;
+      bcol[j] = (FOLD && n < a.Ng) ? a.bias[n] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -417,7 +418,8 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
         for (int e = 0; e < 4; ++e) {
           const int row = rbase + i * 16 + e;
           const int col = cbase + j * 16;
-          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) = from_f32<T>(acc[i][j][e] + bcol[j]);
+          *reinterpret_cast<T*>(smem + row * EROW + col * (int)sizeof(T)) =
+              from_f32<T>(FOLD ? acc[i][j][e] + bcol[j] : acc[i][j][e]);
         }
   }
   __syncthreads();
@@ -460,8 +462,8 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
           for (int j = 0; j < 8; ++j) v.set(j, v.get(j) + r.get(j));
         }
       }
-      if constexpr (MODE == MODE_FWD) {  // folded eval BN: + residual, ReLU (bias already in)
-        if (Add || a.relu) {
+      if constexpr (MODE == MODE_FWD && FOLD) {  // folded eval BN: + residual, ReLU (bias already in)
+        {
           Vec8<T> r;
           if (Add) r.load(Add + orow * a.Ng + n);
 #pragma unroll
@@ -557,8 +559,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[FM
   RowMap rmap;
   rmap.M = a.M;
   rmap.phased = false;
-  conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false, rmap,
-                                                        (int)blockIdx.y);
+  if (MODE == MODE_FWD && a.bias != nullptr)  // ssip_conv_fwd_bias on the register-staged kernel
+    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN, true, true>(a, acc, smem, m0, n0, tm, none, false, rmap,
+                                                                      (int)blockIdx.y);
+  else
+    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN>(a, acc, smem, m0, n0, tm, none, false, rmap,
+                                                          (int)blockIdx.y);
 }
 
 template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN>
@@ -882,7 +888,8 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 // 64-deep k-step covers filter rows 2ks and 2ks+1; k >= R*S*4 reads zeros.
 // POST: DGRAD with the BN-backward epilogue (ssip_conv_dgrad_bn); its
 // operand registers are only allocated in that instantiation.
-template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false>
+template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false,
+          bool FOLD = false>
 __global__ void __launch_bounds__(64 * WMW * WNW,
                                   NSTAGE == 5 ? 2 : glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
     conv_glds_kernel(const ConvArgs a) {
@@ -1366,7 +1373,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   if constexpr (MODE == MODE_DGRAD && POST)
     conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
   else
-    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN, false>(a, acc, smem, m0, n0, tm, post, false, rmap, by);
+    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN, false, FOLD>(a, acc, smem, m0, n0, tm, post, false, rmap,
+                                                                       by);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -1536,7 +1544,7 @@ __device__ __forceinline__ int xtile_off(int px, int slot) { return px * 128 + (
 // wait for the next tile's rows in flight and this tile's output stores
 __device__ __forceinline__ void halo_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }  // one input-row buffer: (TR + 2) * (W + 2) <= 352 pixels
 
-template <int WMW, int WNW>
+template <int WMW, int WNW, bool FOLD = false>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, NT = 64 * NW;
@@ -1732,8 +1740,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
         for (int e = 0; e < 4; ++e) off[i][e] = obase + rowoff[i][e];
       float bcol[FN];  // folded eval BN (FWD): per-column bias
 #pragma unroll
-      for (int jj = 0; jj < FN; ++jj) bcol[jj] = a.bias ? a.bias[jn * BN + cbase + jj * 16] : 0.f;
-      const float lo = a.relu ? 0.f : -__builtin_huge_valf();
+      for (int jj = 0; jj < FN; ++jj) bcol[jj] = FOLD ? a.bias[jn * BN + cbase + jj * 16] : 0.f;
+      const float lo = (FOLD && a.relu) ? 0.f : -__builtin_huge_valf();
       if (a.add) {
         short r[FM][FN][4];
 #pragma unroll
@@ -1749,8 +1757,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
           for (int jj = 0; jj < FN; ++jj)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float t = to_f32(from_f32<T>(acc[i][jj][e] + bcol[jj])) + to_f32(__builtin_bit_cast(T, r[i][jj][e]));
-              const T o = from_f32<T>(fmaxf(t, lo));
+              const float t = to_f32(from_f32<T>(FOLD ? acc[i][jj][e] + bcol[jj] : acc[i][jj][e])) +
+                              to_f32(__builtin_bit_cast(T, r[i][jj][e]));
+              const T o = from_f32<T>(FOLD ? fmaxf(t, lo) : t);
               __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off[i][e] + jj * 32, 0, 0);
             }
       } else {
@@ -1761,7 +1770,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
             for (int e = 0; e < 4; ++e)
               __builtin_amdgcn_raw_buffer_store_b16(
-                  __builtin_bit_cast(short, from_f32<T>(fmaxf(acc[i][jj][e] + bcol[jj], lo))), rsO,
+                  __builtin_bit_cast(short, from_f32<T>(FOLD ? fmaxf(acc[i][jj][e] + bcol[jj], lo) : acc[i][jj][e])), rsO,
                   off[i][e] + jj * 32, 0, 0);
       }
     }
@@ -2594,6 +2603,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(128, 128, 4, 2, 5) X(256, 128, 4, 2, 5) X(128, 256, 2, 4, 5) X(64, 128, 2, 4, 5) X(64, 256, 1, 8, 5)
 
 #define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
+#define SSIP_GLDS_FOLD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2)
 #define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st) {
@@ -2636,6 +2646,18 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
       }
     }
     if constexpr (MODE == MODE_FWD) {
+      if (pl.args.bias != nullptr) {  // folded eval BN epilogue: the default tiles only
+#define SSIP_GLDS_GOF(BM_, BN_, WM_, WN_, ST_)                                                                \
+  if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, false, true>), pl.grid,        \
+                       dim3(64 * WM_ * WN_), 0, st, pl.args);                                                 \
+    return ::ssip::check_launch("conv_glds_fold");                                                            \
+  }
+        SSIP_GLDS_FOLD(SSIP_GLDS_GOF)
+#undef SSIP_GLDS_GOF
+        ::ssip::set_error("no folded-BN conv kernel for %dx%d/%dx%d/%d", pl.bm, pl.bn, pl.wmw, pl.wnw, pl.stages);
+        return SSIP_ERR_ARG;
+      }
       if (pl.conv1) {
 #define SSIP_GLDS_GO4(BM_, BN_, WM_, WN_, ST_)                                                                \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
@@ -2915,7 +2937,9 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
       return SSIP_ERR_ARG;
     }
   }
-  if (nw == 4)
+  if (bias != nullptr)  // folded eval BN epilogue
+    hipLaunchKernelGGL((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
+  else if (nw == 4)
     hipLaunchKernelGGL((conv_halo_kernel<4, 1>), dim3(hp.G), dim3(256), 0, st, h);
   else if (nw == 8)
     hipLaunchKernelGGL((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);

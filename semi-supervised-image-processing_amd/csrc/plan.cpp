@@ -12,6 +12,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <memory>
 #include <vector>
 
@@ -59,6 +61,8 @@ struct Op {
 
 struct ssip_plan {
   std::vector<Op> ops;
+  std::vector<Op> ilv;               // ops re-ordered stream by stream (interleave_segments)
+  size_t ilv_ops = (size_t)-1;       // ops.size() when ilv was built
   std::vector<uint64_t> slots;
   std::vector<std::unique_ptr<uint8_t[]>> blobs;
   std::vector<hipEvent_t> events;
@@ -144,6 +148,73 @@ int ssip_plan_segments(const ssip_plan* plan) { return plan ? (int)plan->seg_beg
 
 int64_t ssip_plan_num_ops(const ssip_plan* plan) { return plan ? (int64_t)plan->ops.size() : -1; }
 
+}  // extern "C"
+
+namespace {
+
+hipStream_t op_stream(const ssip_plan* plan, const Op& op) {
+  if (op.kind == OP_CALL) return (hipStream_t)(uintptr_t)plan->slots[op.arg0 + kPlanFns[op.fn].nargs - 1];
+  return op.stream;
+}
+
+// Enqueue order of a replay: the recorded order puts ALL of a segment's
+// weak-forward launches (side stream) ahead of the train forward's (main
+// stream), so the host spends the first ~60 launches feeding one stream while
+// the other sits empty.  Within each segment, deal the ops out stream by
+// stream, one per stream per turn, keeping each stream's own order; a wait is
+// held back until the event it waits on has been recorded (issued) -- the
+// device-side order the recording established is unchanged.
+void interleave_segments(ssip_plan* plan) {
+  plan->ilv.clear();
+  plan->ilv.reserve(plan->ops.size());
+  const size_t nseg = plan->seg_begin.size();
+  std::vector<char> recorded(plan->events.size(), 0);
+  for (size_t sg = 0; sg < nseg; ++sg) {
+    const size_t b = plan->seg_begin[sg];
+    const size_t e = sg + 1 < nseg ? plan->seg_begin[sg + 1] : plan->ops.size();
+    std::vector<hipStream_t> streams;
+    std::vector<std::vector<size_t>> q;
+    for (size_t i = b; i < e; ++i) {
+      const hipStream_t st = op_stream(plan, plan->ops[i]);
+      size_t k = 0;
+      while (k < streams.size() && streams[k] != st) ++k;
+      if (k == streams.size()) {
+        streams.push_back(st);
+        q.emplace_back();
+      }
+      q[k].push_back(i);
+    }
+    std::vector<size_t> cur(streams.size(), 0);
+    size_t left = e - b;
+    while (left > 0) {
+      bool progress = false;
+      for (size_t k = 0; k < streams.size(); ++k) {
+        // this stream's next op; events and waits do not count as a turn
+        while (cur[k] < q[k].size()) {
+          const Op& op = plan->ops[q[k][cur[k]]];
+          if (op.kind == OP_WAIT && !recorded[op.event]) break;  // its record is not issued yet
+          plan->ilv.push_back(op);
+          if (op.kind == OP_EVENT) recorded[op.event] = 1;
+          ++cur[k];
+          --left;
+          progress = true;
+          if (op.kind == OP_CALL) break;
+        }
+      }
+      if (!progress) {  // cannot happen for a recorded plan (every wait follows its record); keep the order
+        plan->ilv.assign(plan->ops.begin(), plan->ops.end());
+        plan->ilv_ops = plan->ops.size();
+        return;
+      }
+    }
+  }
+  plan->ilv_ops = plan->ops.size();
+}
+
+}  // namespace
+
+extern "C" {
+
 int ssip_plan_run(ssip_plan* plan, int segment) {
   if (!plan || segment < 0 || segment >= (int)plan->seg_begin.size()) {
     ::ssip::set_error("ssip_plan_run: bad plan or segment %d", segment);
@@ -151,8 +222,13 @@ int ssip_plan_run(ssip_plan* plan, int segment) {
   }
   const size_t b = plan->seg_begin[segment];
   const size_t e = segment + 1 < (int)plan->seg_begin.size() ? plan->seg_begin[segment + 1] : plan->ops.size();
+  // SSIP_PLAN_INTERLEAVE=0: the recorded order (A/B)
+  const char* ev = getenv("SSIP_PLAN_INTERLEAVE");
+  const bool ilv = !(ev && ev[0] == '0');
+  if (ilv && plan->ilv_ops != plan->ops.size()) interleave_segments(plan);
+  const std::vector<Op>& seq = ilv ? plan->ilv : plan->ops;
   for (size_t i = b; i < e; ++i) {
-    const Op& op = plan->ops[i];
+    const Op& op = seq[i];
     switch (op.kind) {
       case OP_CALL: {
         const int rc = kPlanFns[op.fn].call(plan->slots.data() + op.arg0);

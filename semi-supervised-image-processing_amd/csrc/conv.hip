@@ -891,7 +891,8 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false,
           bool FOLD = false>
 __global__ void __launch_bounds__(64 * WMW * WNW,
-                                  NSTAGE == 5 ? 2 : glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
+                                  (NSTAGE == 5 || NSTAGE == 8) ? 2
+                                                                : glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
     conv_glds_kernel(const ConvArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, BK = 64;
@@ -902,9 +903,13 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   constexpr int B_BYTES = WG ? BK * BN * 2 : BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   // NSTAGE 5 = the ping-pong schedule on two LDS buffers (see the main loop)
-  static_assert(NSTAGE == 2 || NSTAGE == 3 || NSTAGE == 5, "2 or 3 LDS stages, or ping-pong");
+  static_assert(NSTAGE == 2 || NSTAGE == 3 || NSTAGE == 5 || NSTAGE == 8, "2 or 3 LDS stages, or ping-pong");
   constexpr bool PP = NSTAGE == 5;
-  constexpr int NBUF = PP ? 2 : NSTAGE;
+  // NSTAGE 8 = the 8-phase ping-pong schedule for 256x256 tiles (see the main loop)
+  constexpr bool PP8 = NSTAGE == 8;
+  static_assert(!PP8 || (BM == 256 && BN == 256 && WMW == 2 && WNW == 4 && !C4 && !POST),
+                "the 8-phase schedule is built for 256x256 FWD / stride-1 DGRAD / WGRAD tiles of 8 waves (2 x 4)");
+  constexpr int NBUF = (PP || PP8) ? 2 : NSTAGE;
   static_assert(!PP || (NW == 8 && !POST), "ping-pong pairs the 8 waves of a workgroup two per SIMD");
   constexpr int IA = A_BYTES / 1024, IB = B_BYTES / 1024;
   constexpr int LA = IA / NW, LB = IB / NW;
@@ -1059,12 +1064,22 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
       const int lc = (lane % CPB) ^ (MTile<T, BN>::swz(row) >> 1);
       const int col = n0 + lc * 8;
       b_row[t] = row;
-      b_ok[t] = col < a.Ng;
-      const int cc = b_ok[t] ? col : 0;
-      const int rs = cc / a.C;
-      b_c[t] = cc - rs * a.C;
-      b_r[t] = rs / a.S;
-      b_s[t] = rs - b_r[t] * a.S;
+      if constexpr (PP8) {
+        // C % 256 == 0 (host): the 256 columns of a tile are one tap, so the
+        // tap and its valid p / q ranges are workgroup-uniform (scalars)
+        const int rs = n0 / a.C;
+        b_ok[t] = true;
+        b_c[t] = n0 - rs * a.C + lc * 8;
+        b_r[t] = rs / a.S;
+        b_s[t] = rs - b_r[t] * a.S;
+      } else {
+        b_ok[t] = col < a.Ng;
+        const int cc = b_ok[t] ? col : 0;
+        const int rs = cc / a.C;
+        b_c[t] = cc - rs * a.C;
+        b_r[t] = rs / a.S;
+        b_s[t] = rs - b_r[t] * a.S;
+      }
     }
   }
 
@@ -1112,7 +1127,15 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   // for which that tap lies inside the image (fixed: the slot's tap is fixed)
   int w_p[LB], w_q[LB], w_plo[LB], w_pn[LB], w_qlo[LB], w_qn[LB];
   uint32_t w_pix[LB];
-  if constexpr (WG) {
+  int u_plo = 0, u_pn = 0, u_qlo = 0, u_qn = 0;  // PP8 WGRAD: the tile's (uniform) tap ranges
+  if constexpr (WG && PP8) {
+    const int rs = n0 / a.C, ur = rs / a.S, us = rs - ur * a.S;
+    const int r0 = a.pad - ur, s0 = a.pad - us;
+    u_plo = r0 > 0 ? (r0 + a.stride - 1) / a.stride : 0;
+    u_pn = max(0, min(a.P, (a.H - 1 + r0) >= 0 ? (a.H - 1 + r0) / a.stride + 1 : 0) - u_plo);
+    u_qlo = s0 > 0 ? (s0 + a.stride - 1) / a.stride : 0;
+    u_qn = max(0, min(a.Q, (a.W - 1 + s0) >= 0 ? (a.W - 1 + s0) / a.stride + 1 : 0) - u_qlo);
+  } else if constexpr (WG) {
 #pragma unroll
     for (int t = 0; t < LB; ++t) {
       const int m = (int)min(mstart + b_row[t], (long)a.Mred - 1);
@@ -1247,7 +1270,182 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   // fused-BN epilogue operands: issued first, landed long before the epilogue
   BnPostRegs<T, BM, BN, 64 * WMW * WNW> post;
   if constexpr (MODE == MODE_DGRAD && POST) post.load(a, m0, n0);
-  if constexpr (PP) {
+  if constexpr (PP8) {
+    // 8-phase ping-pong (cdna_hip_programming.md, "The 256^2 8-phase template"):
+    // waves 0-3 (group 0, rows 0-127) and 4-7 (group 1, rows 128-255; one of
+    // each group per SIMD) run the same phases one barrier apart, so in every
+    // barrier interval one wave per SIMD reads fragments / issues LDS-DMA while
+    // its partner runs 16 MFMAs.  A k-step is 4 phases, one C quadrant each:
+    // (rows 0-63, cols 0-31) (0-63, 32-63) (64-127, 32-63) (64-127, 0-31) of the
+    // wave's 128x64 tile; A fragments are re-read every second phase, B every
+    // phase, so 48 VGPRs hold the operands.
+    // Two LDS buffers (k-step parity), each split into an A and a B region.
+    // Loads run ahead per region: B of k-step t+1 is issued in phase 0 of t
+    // (its region was last read in phase 3 of t-1), A of t+2 in phase 3 of t
+    // (its region was last read in phase 2 of t).  Every phase retires its own
+    // fragment reads (lgkmcnt(0)) before its first barrier, so a region is free
+    // for DMA once the barrier after its last read has passed.  All of k-step
+    // t+1's loads are retired by a counted vmcnt (only A of t+2 stays in flight)
+    // before the barrier that precedes the first read of t+1.
+    const int g = wave >> 2;
+    int nk = ph_ksteps;
+    if constexpr (WG) {
+      const long rem = mend - mstart;
+      nk = rem > 0 ? (int)((rem + BK - 1) / BK) : 0;
+    }
+    int kr_a = 0, ks_a = 0, kcb_a = 0;  // k-position of the next A k-step issued
+    int ks_next_a = 0;  // WGRAD: k-step of the next A issue
+    auto issueA = [&](int stage) {
+      char* As = smem + stage * STAGE;
+      if constexpr (WG) {  // dY rows of the k-step (m-major)
+        const int ks = ks_next_a++;
+        const int mlim = (int)(mend - mstart) - ks * BK;
+        const uint32_t moff = (uint32_t)(ks * BK * a.K * 2);
+        constexpr int CPA = BM / 8, RPA = 64 / CPA;
+#pragma unroll
+        for (int t = 0; t < LA; ++t) {  // K % 256 == 0 (host): every column is inside
+          const int row = RPA * (wave + NW * t) + lane / CPA;
+          // rows of slot t are row_0 + RPA * NW * t, same swizzle: one offset register
+          blds16(rsA, row < mlim ? a_off[0] + (uint32_t)(RPA * NW * t * a.K * 2) + moff : SSIP_OOB,
+                 As + (wave + NW * t) * 1024);
+        }
+        return;
+      }
+      uint32_t toff;
+      int tp;
+      if constexpr (MODE == MODE_FWD) {
+        tp = kr_a * a.S + ks_a;
+        toff = (uint32_t)(((kr_a * a.W + ks_a) * a.C + kcb_a) * 2);
+      } else {
+        tp = kr_a * ph_ns + ks_a;
+        toff = (uint32_t)((kcb_a - (kr_a * a.Q + ks_a) * a.K) * 2);
+      }
+#pragma unroll
+      for (int t = 0; t < LA; ++t) {
+        const bool ok = (a_msk[t] >> tp) & 1u;
+        blds16(rsA, ok ? a_off[t] + toff : SSIP_OOB, As + (wave + NW * t) * 1024);
+      }
+      kcb_a += BK;
+      if (kcb_a >= Cred) {
+        kcb_a = 0;
+        if (++ks_a >= ph_ns) { ks_a = 0; ++kr_a; }
+      }
+    };
+    auto issueB = [&](int ks, int stage) {
+      char* Bs = smem + stage * STAGE + A_BYTES;
+      if constexpr (WG) {  // im2col rows of x, each slot walked one k-step on (calls come in k order)
+        const int mlim = (int)(mend - mstart) - ks * BK;
+        constexpr int CPB = BN / 8, RPB = 64 / CPB;
+        // the slot's output pixel recomputed per k-step (no per-slot walk state:
+        // the 128 accumulators leave no registers for it); tap and channel
+        // chunk are the same for every slot (b_c[0]: rows 16 apart share a swizzle)
+        const int rs = n0 / a.C, ur = rs / a.S, us = rs - ur * a.S;
+#pragma unroll
+        for (int t = 0; t < LB; ++t) {
+          const int row = RPB * (wave + NW * t) + lane / CPB;
+          const int m = min((int)mstart + ks * BK + row, a.Mred - 1);
+          const int n = fdiv(m, a.div_pq);
+          const int rem = m - n * a.P * a.Q;
+          const int pp = fdiv(rem, a.div_q);
+          const int qq = rem - pp * a.Q;
+          const bool ok = row < mlim && (uint32_t)(pp - u_plo) < (uint32_t)u_pn &&
+                          (uint32_t)(qq - u_qlo) < (uint32_t)u_qn;
+          const int hin = pp * a.stride - a.pad + ur, win = qq * a.stride - a.pad + us;
+          const uint32_t pix = (uint32_t)(((n * a.H + hin) * a.W + win) * a.C + b_c[0]) * 2u;
+          blds16(rsB, ok ? pix : SSIP_OOB, Bs + (wave + NW * t) * 1024);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < LB; ++t) blds16(rsB, b_off[t] + (uint32_t)(ks * BK * 2), Bs + (wave + NW * t) * 1024);
+      }
+    };
+    Frag<T> fa[2][4], fb[2][2];
+    auto readA = [&](int buf, int mi) {
+      const char* As = smem + buf * STAGE;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if constexpr (WG) read_mfrag<BM>(fa[h][i], As, wm * 128 + (mi * 4 + i) * 16, lane, h);
+          else read_kfrag(fa[h][i], As, wm * 128 + (mi * 4 + i) * 16 + (lane & 15), lane >> 4, h);
+        }
+    };
+    auto readB = [&](int buf, int nj) {
+      const char* Bs = smem + buf * STAGE + A_BYTES;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (WG) read_mfrag<BN>(fb[h][j], Bs, wn * 64 + (nj * 2 + j) * 16, lane, h);
+          else read_kfrag(fb[h][j], Bs, wn * 64 + (nj * 2 + j) * 16 + (lane & 15), lane >> 4, h);
+        }
+    };
+#define SSIP_PP8_MFMA(MI, NJ)                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    __builtin_amdgcn_s_setprio(1);                                                  \
+    _Pragma("unroll") for (int h = 0; h < 2; ++h)                                   \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                   \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                   \
+        mma(acc[(MI) * 4 + i][(NJ) * 2 + j], fa[h][i], fb[h][j]);                   \
+    __builtin_amdgcn_s_setprio(0);                                                  \
+    __builtin_amdgcn_sched_barrier(0);
+#define SSIP_PP8_SYNC(ASM)                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    asm volatile(ASM ::: "memory");                                                 \
+    __builtin_amdgcn_sched_barrier(0);
+    if (nk > 0) {
+      issueA(0);
+      issueB(0, 0);
+      if (nk > 1) {
+        issueA(1);
+        wait_vm_barrier<LA>();
+      } else {
+        wait_vm_barrier<0>();
+      }
+      if (g) { SSIP_PP8_SYNC("s_barrier") }
+      for (int t = 0; t < nk; ++t) {
+        const int buf = t & 1;
+        // phase 0: quadrant (0, 0); B of k-step t+1 into the other buffer
+        readA(buf, 0);
+        readB(buf, 0);
+        if (t + 1 < nk) issueB(t + 1, buf ^ 1);
+        SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
+        SSIP_PP8_MFMA(0, 0)
+        SSIP_PP8_SYNC("s_barrier")
+        // phase 1: (0, 1)
+        readB(buf, 1);
+        SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
+        SSIP_PP8_MFMA(0, 1)
+        SSIP_PP8_SYNC("s_barrier")
+        // phase 2: (1, 1)
+        readA(buf, 1);
+        SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
+        SSIP_PP8_MFMA(1, 1)
+        SSIP_PP8_SYNC("s_barrier")
+        // phase 3: (1, 0); A of k-step t+2 into this buffer's A region; k-step
+        // t+1 retired (counted) before the barrier that ends this phase for
+        // both groups (group 1: its first barrier, group 0: its second)
+        readB(buf, 0);
+        const bool more = t + 2 < nk;
+        if (more) issueA(buf);
+        if (g) {
+          if (more) { SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(4)\n\ts_barrier") }
+          else { SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)\n\ts_barrier") }
+          SSIP_PP8_MFMA(1, 0)
+          SSIP_PP8_SYNC("s_barrier")
+        } else {
+          SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
+          SSIP_PP8_MFMA(1, 0)
+          if (more) { SSIP_PP8_SYNC("s_waitcnt vmcnt(4)\n\ts_barrier") }
+          else { SSIP_PP8_SYNC("s_waitcnt vmcnt(0)\n\ts_barrier") }
+        }
+      }
+      if (!g) { SSIP_PP8_SYNC("s_barrier") }
+    }
+#undef SSIP_PP8_MFMA
+#undef SSIP_PP8_SYNC
+    static_assert(!PP8 || LA == 4, "vmcnt(4) above counts one k-step of A loads per wave");
+  } else if constexpr (PP) {
     // Ping-pong (MI355X_MICROARCH.md "Two waves per SIMD"): waves 0-3
     // (group 0) and 4-7 (group 1; one on each SIMD beside a group-0 wave)
     // run the same k-steps one barrier interval apart, so in every interval
@@ -2559,7 +2757,8 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
       splits = std::min(max_splits, ceil_div(std::max(1, atoi(e)), tiles));
     } else if (pl.stages > 0) {
       const int nt = 64 * pl.wmw * pl.wnw;
-      const int lds = std::max(2, pl.stages) * 64 * (pl.bm + pl.bn) * 2;
+      const int nbuf = (pl.stages == 5 || pl.stages == 8) ? 2 : std::max(2, pl.stages);
+      const int lds = nbuf * 64 * (pl.bm + pl.bn) * 2;
       const int per_cu = std::max(1, std::min(2048 / nt, 163840 / lds));
       const long slots = (long)device_cus() * per_cu;
       double best = 1e30;
@@ -2593,14 +2792,15 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
   X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)             \
   X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2) X(256, 256, 4, 2, 2) X(512, 64, 8, 1, 2)      \
-  X(256, 128, 4, 2, 5) X(512, 64, 8, 1, 5) X(128, 128, 4, 2, 5) X(256, 64, 8, 1, 5)
+  X(256, 128, 4, 2, 5) X(512, 64, 8, 1, 5) X(128, 128, 4, 2, 5) X(256, 64, 8, 1, 5) X(256, 256, 2, 4, 8)
 #define SSIP_GLDS_WG(X)                                                                                      \
   X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
   X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
   X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
   X(64, 128, 1, 8, 2) X(128, 128, 4, 4, 3) X(64, 128, 2, 4, 3) X(128, 64, 2, 4, 3) X(256, 128, 4, 4, 2)    \
   X(128, 256, 2, 2, 2) X(256, 128, 2, 2, 2) X(64, 256, 1, 2, 2) X(256, 256, 2, 2, 2) X(128, 128, 2, 4, 5)    \
-  X(128, 128, 4, 2, 5) X(256, 128, 4, 2, 5) X(128, 256, 2, 4, 5) X(64, 128, 2, 4, 5) X(64, 256, 1, 8, 5)
+  X(128, 128, 4, 2, 5) X(256, 128, 4, 2, 5) X(128, 256, 2, 4, 5) X(64, 128, 2, 4, 5) X(64, 256, 1, 8, 5) \
+  X(256, 256, 2, 4, 8)
 
 #define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
 #define SSIP_GLDS_FOLD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2)
@@ -2622,6 +2822,10 @@ static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st
 
 template <int MODE>
 static int launch_glds(const Plan& pl, hipStream_t st) {
+  SSIP_REQUIRE(pl.stages != 8 || !pl.args.phased, SSIP_ERR_ARG,
+               "the 8-phase kernel has no stride-2 dgrad phase split");
+  SSIP_REQUIRE(pl.stages != 8 || MODE != MODE_WGRAD || (pl.args.C % 256 == 0 && pl.args.K % 256 == 0), SSIP_ERR_ARG,
+               "the 8-phase wgrad needs C and K multiples of 256 (one tap per 256-column tile)");
 #define SSIP_GLDS_GO(BM_, BN_, WM_, WN_, ST_)                                                                 \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
     hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
@@ -2681,7 +2885,18 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
 template <int MODE, typename T>
 static int launch_conv(const Plan& pl, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
-    if (pl.stages > 0) return launch_glds<MODE>(pl, st);
+    if (pl.stages > 0) {
+      // SSIP_DIAG (timing experiments only): 1 = drop the A operand's loads,
+      // 2 = drop B's (zero-extent buffer resources read zeros; results are wrong)
+      static const int diag = getenv("SSIP_DIAG") ? atoi(getenv("SSIP_DIAG")) : 0;
+      if (diag) {
+        Plan p2 = pl;
+        if (diag & 1) p2.args.a_bytes = 0;
+        if (diag & 2) p2.args.b_bytes = 0;
+        return launch_glds<MODE>(p2, st);
+      }
+      return launch_glds<MODE>(pl, st);
+    }
   }
 #define SSIP_LAUNCH(BM_, BN_, WM_, WN_, C1_)                                                                  \
   {                                                                                                           \

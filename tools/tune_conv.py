@@ -17,14 +17,14 @@ FD = [(256, 128, 4, 2, 3), (256, 128, 4, 2, 2), (256, 64, 4, 1, 2), (256, 64, 4,
       (256, 128, 4, 4, 2), (128, 64, 4, 2, 3), (128, 128, 4, 4, 3), (256, 128, 4, 4, 3),
       (256, 128, 2, 2, 2), (512, 64, 4, 1, 2), (256, 256, 2, 2, 2), (256, 256, 4, 2, 2), (512, 64, 8, 1, 2),
       (256, 128, 4, 2, 5), (512, 64, 8, 1, 5), (128, 128, 4, 2, 5), (256, 64, 8, 1, 5),
-      (256, 128, 4, 2, 0), (256, 64, 4, 2, 0), (128, 128, 2, 2, 0), (128, 64, 2, 2, 0)]
+      (256, 128, 4, 2, 0), (256, 64, 4, 2, 0), (128, 128, 2, 2, 0), (128, 64, 2, 2, 0), (256, 256, 2, 4, 8)]
 WG = [(128, 128, 2, 2, 2), (128, 128, 2, 2, 3), (128, 128, 2, 4, 2), (128, 128, 2, 4, 3), (128, 64, 2, 2, 2),
       (128, 64, 2, 2, 3), (128, 64, 2, 1, 2), (64, 128, 1, 4, 2), (64, 128, 1, 4, 3), (64, 128, 1, 2, 2),
       (64, 128, 1, 8, 3), (128, 128, 4, 2, 2), (128, 128, 4, 4, 2), (128, 64, 2, 4, 2), (64, 128, 2, 4, 2),
       (64, 128, 1, 8, 2), (128, 128, 4, 4, 3), (64, 128, 2, 4, 3), (128, 64, 2, 4, 3), (256, 128, 4, 4, 2),
       (128, 256, 2, 2, 2), (256, 128, 2, 2, 2), (64, 256, 1, 2, 2), (256, 256, 2, 2, 2),
       (128, 128, 2, 4, 5), (128, 128, 4, 2, 5), (256, 128, 4, 2, 5), (128, 256, 2, 4, 5), (64, 128, 2, 4, 5),
-      (64, 256, 1, 8, 5),
+      (64, 256, 1, 8, 5), (256, 256, 2, 4, 8),
       (128, 128, 2, 2, 0), (128, 64, 2, 2, 0), (64, 128, 2, 2, 0)]
 
 
@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--modes", default="fdw", help="passes to tune: any of f, d, w")
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--wg", default="", help="wgrad configs 'bm,bn,wm,wn,st;...' (default: the built-in list)")
+    ap.add_argument("--fd", default="", help="fwd/dgrad configs 'bm,bn,wm,wn,st;...' (default: the built-in list)")
+    ap.add_argument("--no-check", action="store_true", help="skip the result check (SSIP_DIAG ablation builds)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
@@ -65,6 +67,7 @@ def main():
     part = torch.empty(8 << 20, dtype=torch.float32, device=dev)
     res = []
     wg_cfgs = [tuple(int(v) for v in c.split(",")) for c in args.wg.split(";") if c] or WG
+    fd_cfgs = [tuple(int(v) for v in c.split(",")) for c in args.fd.split(";") if c] or FD
     want = set(args.shapes.split(",")) if args.shapes else None
     for nm, g in shapes(args.batch):
         if want is not None and nm not in want:
@@ -77,8 +80,8 @@ def main():
         dx = torch.empty_like(x)
         dw = torch.empty(g.K, g.C, g.R, g.S, device=dev, dtype=torch.float32)
         runs = {
-            "f": (FD, lambda: ops.conv_fwd(g, x, w, y, part), y),
-            "d": (FD, lambda: ops.conv_dgrad(g, dy, wc, dx), dx),
+            "f": (fd_cfgs, lambda: ops.conv_fwd(g, x, w, y, part), y),
+            "d": (fd_cfgs, lambda: ops.conv_dgrad(g, dy, wc, dx), dx),
             "w": (wg_cfgs, lambda: ops.conv_wgrad(g, dy, x, dw, False, ws), dw),
         }
         for mode, (cfgs, fn, out) in runs.items():
@@ -97,7 +100,7 @@ def main():
                 except RuntimeError as e:  # configuration not valid for this shape
                     row["cfg"][str(c)] = str(e)[:60]
                     continue
-                err = (out.float() - ref).abs().max().item() / scale
+                err = 0.0 if args.no_check else (out.float() - ref).abs().max().item() / scale
                 if not err < 2e-2:
                     row["cfg"][str(c)] = f"MISMATCH rel err {err:.3g}"
                     print(f"  {nm} {mode} {c}: MISMATCH rel err {err:.3g}", flush=True)

@@ -85,7 +85,11 @@ class AdamW(torch.optim.Optimizer):
         return runs, loose
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0):
+    def step(self, closure=None, grad_scale: float = 1.0, only=None, skip=None, sched_step: bool = True):
+        """One AdamW update.  ``only`` / ``skip``: sets of id(param) restricting
+        the update to a subset (a step split around a pending gradient, see
+        SemiStep); the later parts of a split pass ``sched_step=False`` so the
+        device schedule advances once per step."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -95,12 +99,13 @@ class AdamW(torch.optim.Optimizer):
         self._ensure_flat_state()
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
-            params = [p for p in group["params"] if p.grad is not None]
+            params = [p for p in group["params"] if p.grad is not None and (only is None or id(p) in only)
+                      and (skip is None or id(p) not in skip)]
             if not params:
                 continue
             runs, loose = self._runs(gi, params)
             if self._sched is not None:
-                self._step_device(gi, group, params, runs, loose, grad_scale)
+                self._step_device(gi, group, params, runs, loose, grad_scale, sched_step)
                 continue
             # per-parameter state (views into the flat state for arena params)
             for p in params:
@@ -142,7 +147,7 @@ class AdamW(torch.optim.Optimizer):
                 st["exp_avg_sq"] = torch.zeros_like(p)
         return st
 
-    def _step_device(self, gi, group, params, runs, loose, grad_scale):
+    def _step_device(self, gi, group, params, runs, loose, grad_scale, sched_step=True):
         b1, b2 = group["betas"]
         sched = self._sched[gi]
         if group["lr"] != self._sched_lr[gi]:  # an LR scheduler moved it (host decision, eager only)
@@ -150,7 +155,8 @@ class AdamW(torch.optim.Optimizer):
             self._sched_lr[gi] = group["lr"]
         for p in params:
             self._init_state(p)
-        ops.adamw_sched_step(sched, b1, b2)
+        if sched_step:
+            ops.adamw_sched_step(sched, b1, b2)
         for off, n, ps in runs:
             ops.adamw_dev(self.arena.flat[off:off + n], self.arena.grad[off:off + n],
                           self._flat_state[0][off:off + n], self._flat_state[1][off:off + n], sched,

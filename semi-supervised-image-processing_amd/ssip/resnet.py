@@ -204,6 +204,14 @@ class SSIPResNet(nn.Module):
         self._bn_epoch = 0
         self._arena = None
         self.embedding_only = False
+        # backward tail (single process, SemiStep): leave the stem wgrad (the
+        # last kernel of the backward, on the wgrad side stream) unjoined; the
+        # main stream only waits for the wgrads before it, so the optimizer
+        # and the compute-dtype weight refresh of every other parameter overlap
+        # it.  The caller must ops.wait_stream(main, model.take_pending_side())
+        # before it reads conv1.weight.grad.
+        self.defer_stem_wgrad_join = False
+        self._pending_side = None
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -247,6 +255,12 @@ class SSIPResNet(nn.Module):
         if self._arena is None or not self._arena.valid():
             self._arena = ParamArena(list(self.parameters()))
         return self._arena
+
+    def take_pending_side(self):
+        """The side stream whose stem wgrad the last backward left unjoined
+        (defer_stem_wgrad_join), or None; clears it."""
+        s, self._pending_side = self._pending_side, None
+        return s
 
     def prepare_weights(self, need_t: bool = True, force: bool = False) -> None:
         """Refresh the compute-dtype conv weight copies now (one launch) so a
@@ -572,10 +586,15 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
         _backward_impl(model, sv, dlogits, None, None)
         return
     main = torch.cuda.current_stream(dlogits.device)
+    model._pending_side = None
+    deferred = False
     try:
-        _backward_impl(model, sv, dlogits, main, side)
+        deferred = _backward_impl(model, sv, dlogits, main, side)
     finally:
-        ops.wait_stream(main, side)
+        if deferred:
+            model._pending_side = side
+        else:
+            ops.wait_stream(main, side)
 
 
 def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, side):
@@ -814,6 +833,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     # dy pass) where the geometry allows: ssip_stem_bwd_wgrad
     fused = (w1.requires_grad and (mp.kernel_size, mp.stride, mp.padding) == (3, 2, 1)
              and ops.stem_bwd_wgrad_supported(stem.geom, dt))
+    defer = bool(fused and side is not None and hook is None and model.defer_stem_wgrad_join)
     dy1 = None if fused else torch.empty_like(stem.y)
     coef1 = coef_buf[: 3 * C1] if not fused else torch.empty(3 * C1, device=dev, dtype=torch.float32)
     ops.stem_pool_bn_bwd(N, P1, Q1, C1, mp.kernel_size, mp.stride, mp.padding, dz, sv.pool_idx, stem.y,
@@ -827,14 +847,19 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             ops.stem_bwd_wgrad(*args)
         else:
             ops.wait_stream(side, main)
+            if defer:
+                # main waits for every wgrad queued so far, not for this one
+                ops.wait_stream(main, side)
             with torch.cuda.stream(side):
                 ops.stem_bwd_wgrad(*args)
             for t in (dz, coef1):
                 t.record_stream(side)
     else:
+        defer = False
         conv_wgrad(stem, dy1)
     if hook is not None:
         hook([model.conv1.weight, model.bn1.weight, model.bn1.bias])
+    return defer
 
 
 def _ds_dgrad_fusable(g: ConvGeom, gds: ConvGeom) -> bool:

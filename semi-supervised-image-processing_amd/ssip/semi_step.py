@@ -21,6 +21,7 @@ Step (per rank, B_l labelled + B_u unlabelled uint8 images resident in HBM):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -35,6 +36,19 @@ from .resnet import DeviceImages, SSIPResNet
 @dataclass
 class StepStats:
     loss: torch.Tensor        # [4] total, L_l, L_u, mask count (device)
+
+
+def _common_base(params):
+    """The tensor the view parameters are consecutive row ranges of, or None."""
+    b = params[0]._base
+    if b is None or not b.is_contiguous() or b.dim() != 2:
+        return None
+    o = 0
+    for p in params:
+        if p._base is not b or p.data_ptr() != b[o:].data_ptr():
+            return None
+        o += p.shape[0]
+    return b if o == b.shape[0] else None
 
 
 class SemiStep:
@@ -75,8 +89,13 @@ class SemiStep:
             raise ValueError("SemiStep: graph and plan are alternatives")
         self.plan = plan
         self._plan = None
+        self._static_pbase = None
         if graph or plan:
             self.opt.use_device_schedule()
+        # single process, no graph capture: the optimizer overlaps the stem
+        # wgrad at the end of the backward (a graph capture needs every forked
+        # stream joined; a gradient bucketer reduces conv1's gradient itself)
+        model.defer_stem_wgrad_join = bucketer is None and not graph and os.environ.get("SSIP_DEFER_STEM") != "0"
 
     def _side_stream(self, dev):
         if self._side is None:
@@ -84,11 +103,20 @@ class SemiStep:
         return self._side
 
     def draw_params(self, Bl: int, Bu: int):
-        """Per-sample view parameters (host RNG, like a DataLoader worker)."""
+        """Per-sample view parameters (host RNG, like a DataLoader worker):
+        (labelled weak, unlabelled weak, unlabelled strong) as views of one
+        pinned buffer, so a step moves them to the device in one copy."""
         s = self.size
-        return (draw_params_batch(Bl, s, False, self.gen).pin_memory(),
-                draw_params_batch(Bu, s, False, self.gen).pin_memory(),
-                draw_params_batch(Bu, s, True, self.gen).pin_memory())
+        parts = (draw_params_batch(Bl, s, False, self.gen), draw_params_batch(Bu, s, False, self.gen),
+                 draw_params_batch(Bu, s, True, self.gen))
+        buf = torch.cat(parts).pin_memory()
+        return (buf[:Bl], buf[Bl:Bl + Bu], buf[Bl + Bu:])
+
+    def input_slots(self):
+        """The device buffers a recorded plan reads its batch from
+        (x_l, y_l, x_u): an input pipeline that writes the next batch here
+        spares the step its copy-in.  None before the plan is recorded."""
+        return None if self._plan is None else self._static[:3]
 
     # the three pieces of steps 1-5; each runs on the current stream and is
     # capturable (no host sync, no host-side value that changes per step)
@@ -159,8 +187,36 @@ class SemiStep:
         out = self._fwd_bwd(x_l, y_l, x_u, pl, pw, ps)
         scale = self.bucketer.finish() if self.bucketer is not None else 1.0
         # 6. optimizer
-        self.opt.step(grad_scale=scale)
+        self._optimizer_step(scale)
         return StepStats(loss=out)
+
+    def _dev_params(self, params, dev):
+        """Device copies of the view parameters; views of one device buffer
+        when the host ones are views of one buffer (one copy per replay)."""
+        base = _common_base(params)
+        self._static_pbase = None
+        if base is None:
+            return tuple(p.to(dev) for p in params)
+        self._static_pbase = base.to(dev)
+        out, o = [], 0
+        for p in params:
+            out.append(self._static_pbase[o:o + p.shape[0]])
+            o += p.shape[0]
+        return tuple(out)
+
+    def _optimizer_step(self, scale: float) -> None:
+        """AdamW; with the stem wgrad still running on the side stream
+        (defer_stem_wgrad_join) every other parameter is updated and its
+        compute-dtype copies refreshed first, beside it, then conv1."""
+        m = self.model
+        pend = m.take_pending_side()
+        if pend is None:
+            self.opt.step(grad_scale=scale)
+            return
+        late = {id(m.conv1.weight)}
+        self.opt.step(grad_scale=scale, skip=late)
+        ops.wait_stream(torch.cuda.current_stream(), pend)
+        self.opt.step(grad_scale=scale, only=late, sched_step=False)
 
     # ------------------------------------------------------------------
     # launch-plan path (ssip/plan.py): record one step, replay it from C++
@@ -178,18 +234,24 @@ class SemiStep:
 
         dev = x_l.device
         if self._plan is None:
-            self._static = (x_l.clone(), y_l.clone(), x_u.clone()) + tuple(p.to(dev) for p in params)
+            self._static = (x_l.clone(), y_l.clone(), x_u.clone()) + self._dev_params(params, dev)
             plan = Plan()
             scale = 1.0 / self.bucketer.world if self.bucketer is not None else 1.0
             with plan:
                 out = self._fwd_bwd(*self._static)
                 if self.bucketer is not None:
                     ops.host_callback(self._finish_buckets)
-                self.opt.step(grad_scale=scale)
+                self._optimizer_step(scale)
             self._plan, self._plan_out = plan, out
             return StepStats(loss=out)
-        for dst, src in zip(self._static, (x_l, y_l, x_u) + tuple(params)):
+        for dst, src in zip(self._static[:3], (x_l, y_l, x_u)):
             if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        base = _common_base(params)
+        if base is not None and self._static_pbase is not None and base.shape == self._static_pbase.shape:
+            self._static_pbase.copy_(base, non_blocking=True)
+        else:
+            for dst, src in zip(self._static[3:], params):
                 dst.copy_(src, non_blocking=True)
         if self.bucketer is not None:
             self.bucketer.reset()

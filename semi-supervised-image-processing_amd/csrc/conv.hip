@@ -2444,6 +2444,7 @@ struct StemBwArgs {
   float* slab;          // [G][64][224]
   uint32_t x_bytes, y_bytes, dp_bytes, ix_bytes;
   int N, H, W, P, Q, P2, Q2, tiles;
+  int diag;  // SSIP_STEM_DIAG (timing experiments only): 1 = skip the dy pass, 2 = skip the MFMAs, 8 = per-pixel gather
 };
 
 constexpr int SBW_Y = 28 * 1024, SBW_DP = 14 * 1024, SBW_IX = 7 * 1024;
@@ -2520,13 +2521,75 @@ __global__ void __launch_bounds__(512, 2) conv_stem_bwd_wgrad_kernel(const StemB
     first = false;
     halo_lds_barrier();  // this tile's inputs landed; the dy image and the other buffer are free
     if (u + 1 < u1) issue(u + 1, Bn);
-    {
+    if (!(a.diag & 1)) {
       // ---- dy for the tile's 224 output pixels, into the m-major MTile image
       const int R0 = u * 2;
       const int h0 = R0 - (R0 / a.P) * a.P, T0 = h0 >> 1;
       const char* Ys = Bc + STEM_XBUF;
       const char* Ps = Ys + SBW_Y;
       const char* Is = Ps + SBW_DP;
+      if (!(a.diag & 8)) {
+        // 2x2 pixel blocks: rows (h0, h0+1) x columns (2l, 2l+1), one 8-channel
+        // chunk per thread.  h0 is even, so row h0 lies only in pooled row T0
+        // (window row 1), row h0+1 in T0 (row 2) and T0+1 (row 0); likewise
+        // column 2l in window l (column 1), 2l+1 in l (2) and l+1 (0).  The
+        // block's four windows are read once and every (window, pixel) pair
+        // is tested without branches; contributions are added in the same
+        // (p, q)-ascending order as the per-pixel gather below.
+        const int QH = a.Q >> 1;
+        if (tid < QH * 8) {
+          const int l = tid >> 3;
+          const bool q1 = l + 1 < a.Q2, p1 = T0 + 1 < a.P2;
+          const uint64_t NOHIT = ~0ull;  // no argmax byte is 255
+          uint64_t k00, k01 = NOHIT, k10 = NOHIT, k11 = NOHIT;
+          Vec8<T> g00, g01, g10, g11;
+          k00 = *reinterpret_cast<const uint64_t*>(Is + l * 64 + c0);
+          g00.v = *reinterpret_cast<const i32x4*>(Ps + l * 128 + c0 * 2);
+          g01.v = g10.v = g11.v = (i32x4){0, 0, 0, 0};
+          if (q1) {
+            k01 = *reinterpret_cast<const uint64_t*>(Is + (l + 1) * 64 + c0);
+            g01.v = *reinterpret_cast<const i32x4*>(Ps + (l + 1) * 128 + c0 * 2);
+          }
+          if (p1) {
+            k10 = *reinterpret_cast<const uint64_t*>(Is + (a.Q2 + l) * 64 + c0);
+            g10.v = *reinterpret_cast<const i32x4*>(Ps + (a.Q2 + l) * 128 + c0 * 2);
+            if (q1) {
+              k11 = *reinterpret_cast<const uint64_t*>(Is + (a.Q2 + l + 1) * 64 + c0);
+              g11.v = *reinterpret_cast<const i32x4*>(Ps + (a.Q2 + l + 1) * 128 + c0 * 2);
+            }
+          }
+          float dz[4][8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int b00 = (int)((k00 >> (8 * e)) & 0xff), b01 = (int)((k01 >> (8 * e)) & 0xff);
+            const int b10 = (int)((k10 >> (8 * e)) & 0xff), b11 = (int)((k11 >> (8 * e)) & 0xff);
+            const float v00 = g00.get(e), v01 = g01.get(e), v10 = g10.get(e), v11 = g11.get(e);
+            float d;
+            d = 0.f; if (b00 == 4) d += v00;
+            dz[0][e] = d;
+            d = 0.f; if (b00 == 5) d += v00; if (b01 == 3) d += v01;
+            dz[1][e] = d;
+            d = 0.f; if (b00 == 7) d += v00; if (b10 == 1) d += v10;
+            dz[2][e] = d;
+            d = 0.f; if (b00 == 8) d += v00; if (b01 == 6) d += v01; if (b10 == 2) d += v10; if (b11 == 0) d += v11;
+            dz[3][e] = d;
+          }
+#pragma unroll
+          for (int px = 0; px < 4; ++px) {
+            const int m = (px >> 1) * a.Q + 2 * l + (px & 1);
+            Vec8<T> yy, o;
+            yy.v = *reinterpret_cast<const i32x4*>(Ys + m * 128 + c0 * 2);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float yv = yy.get(e);
+              const float t = __builtin_fmaf(yv, sc[e], sh[e]);
+              const float d = (t > 0.f ? t : 0.f) > 0.f ? dz[px][e] : 0.f;
+              o.set(e, ca[e] * d + cb[e] * yv + ck[e]);
+            }
+            *reinterpret_cast<i32x4*>(Dimg + m * 128 + ((cc ^ ((m & 3) << 1)) << 4)) = o.v;
+          }
+        }
+      } else
       for (int id = tid; id < MR * 8; id += 512) {
         const int m = id >> 3;
         const int j = m >= a.Q ? 1 : 0, w = m - j * a.Q, h = h0 + j;
@@ -2569,7 +2632,7 @@ __global__ void __launch_bounds__(512, 2) conv_stem_bwd_wgrad_kernel(const StemB
     halo_lds_barrier();  // dy image complete
     const char* Xs = Bc;
 #pragma unroll
-    for (int ks = 0; ks < MR / 32; ++ks) {
+    for (int ks = 0; ks < ((a.diag & 2) ? 0 : MR / 32); ++ks) {
       Frag<T> fa[2], fb[4];
 #pragma unroll
       for (int x = 0; x < 2; ++x) read_tfrag(fa[x], Dimg, 32 * ks, (2 * wm + x) * 16, lane);
@@ -2673,6 +2736,12 @@ static void choose_glds(int mode, const ConvArgs& a, Plan& pl) {
   // (ResNet-18 layer3: 62.7 vs 69.1 us, profiles/r1_conv_tune.txt)
   if (mode == MODE_FWD && a.Ng % 256 == 0 && (long)ceil_div(a.M, 256) * (a.Ng / 256) >= 160) {
     pl.bm = 256; pl.bn = 256;
+  } else if (mode == MODE_FWD && a.Ng % 128 == 0 && (long)ceil_div(a.M, 128) * (a.Ng / 128) <= device_cus()) {
+    // at most one 128x128 tile per CU (the weak forward's layer4 at batch 128:
+    // 196 tiles): one workgroup of 16 waves (32x32 wave tiles) and a 3-deep
+    // ring per CU instead of 8 waves that leave every second slot empty
+    // (l4.3x3 42.4 vs 50.2 us, l4.3x3s2 24.1 vs 26.7, profiles/r2_tune_fwd_b128.txt)
+    pl.wnw = 4; pl.stages = 3;
   }
 }
 
@@ -2803,7 +2872,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   X(256, 256, 2, 4, 8)
 
 #define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
-#define SSIP_GLDS_FOLD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2)
+#define SSIP_GLDS_FOLD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2) X(128, 128, 4, 4, 3)
 #define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st) {
@@ -3442,6 +3511,11 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
   h.dp_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64 * 2);
   h.ix_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64);
   h.N = d->N; h.H = d->H; h.W = d->W; h.P = d->P; h.Q = d->Q; h.P2 = P2; h.Q2 = Q2; h.tiles = hp.tiles;
+  {
+    static const int diag = getenv("SSIP_STEM_DIAG") ? atoi(getenv("SSIP_STEM_DIAG")) : 0;
+    h.diag = diag & 11;
+    if (diag & 4) h.x_bytes = h.y_bytes = h.dp_bytes = h.ix_bytes = 0;  // zero-extent: no memory traffic
+  }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv_stem_bwd_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
   int rc = ::ssip::check_launch("conv_stem_bwd_wgrad");

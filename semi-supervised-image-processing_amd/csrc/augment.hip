@@ -60,13 +60,16 @@ __global__ void augment_kernel(int B, const uint8_t* __restrict__ src, long src_
                                const int* __restrict__ bounds_v, const int* __restrict__ coeffs_v,
                                const ssip_aug_param* __restrict__ params, float m0, float m1, float m2, float s0,
                                float s1, float s2, int opad, T* __restrict__ out) {
+  // one workgroup per output row (grid Hp x B): sample index and row are
+  // workgroup-uniform (the sample's parameters are scalar loads), no 64-bit
+  // index division per pixel
   const int Hp = Ho + 2 * opad, Wp = Wo + 2 * opad;
-  const long total = (long)B * Hp * Wp;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int x = (int)(i % Wp) - opad;
-    const long t = i / Wp;
-    const int y = (int)(t % Hp) - opad;
-    const int b = (int)(t / Hp);
+  const int y = (int)blockIdx.x - opad;
+  const int b = (int)blockIdx.y;
+  const ssip_aug_param pa = params ? params[b] : ssip_aug_param{};
+  for (int xp = threadIdx.x; xp < Wp; xp += blockDim.x) {
+    const long i = ((long)b * Hp + blockIdx.x) * Wp + xp;
+    const int x = xp - opad;
     if (x < 0 || x >= Wo || y < 0 || y >= Ho) {  // zero border of a pre-padded stem input
       Vec4Px<T> z;
 #pragma unroll
@@ -74,7 +77,6 @@ __global__ void augment_kernel(int B, const uint8_t* __restrict__ src, long src_
       *reinterpret_cast<Vec4Px<T>*>(out + i * 4) = z;
       continue;
     }
-    const ssip_aug_param pa = params ? params[b] : ssip_aug_param{};
     const int xr = x + cx, yr = y + cy;
     int xin = xr, yin = yr;
     bool inside = true;
@@ -181,9 +183,13 @@ int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stri
   SSIP_REQUIRE(src_w == Wr && (ksize_v > 0 ? (bounds_v && coeffs_v) : src_h == Hr), SSIP_ERR_ARG,
                "ssip_augment_u8: source geometry does not match the resize plan");
   SSIP_REQUIRE(out_pad >= 0 && out_pad <= 8, SSIP_ERR_ARG, "ssip_augment_u8: out_pad must be 0..8");
-  const long total = (long)B * (Ho + 2 * out_pad) * (Wo + 2 * out_pad);
+  SSIP_REQUIRE((long)B * (Ho + 2 * out_pad) < 65536l * 65536l && B < 65536, SSIP_ERR_ARG,
+               "ssip_augment_u8: batch too large");
+  const int wp = Wo + 2 * out_pad;
+  const dim3 grid((unsigned)(Ho + 2 * out_pad), (unsigned)B);
+  const dim3 block((unsigned)(wp >= 256 ? 256 : ((wp + 63) / 64) * 64));
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(augment_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, src,
+    hipLaunchKernelGGL(augment_kernel<T>, grid, block, 0, (hipStream_t)stream, B, src,
                        (long)src_batch_stride, src_h, src_w, Hr, Wr, Ho, Wo, crop_x, crop_y, ksize_v, bounds_v,
                        coeffs_v, params, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], out_pad, (T*)out);
   });

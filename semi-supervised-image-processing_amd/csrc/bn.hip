@@ -241,27 +241,26 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, 
     }
   };
   if (rsub < rpi) {
+    // four rows in flight per thread, accumulated in plain-walk order
+    constexpr int U = 4;
     long r = r0 + rsub;
-    for (; r + rpi < r1; r += 2 * rpi) {
-      Vec8<T> g0, g1, z0, z1, a0, a1, b0, b1;
-      uint32_t m0 = 0, m1 = 0;
-      g0.load(dz + r * C + c0);
-      g1.load(dz + (r + rpi) * C + c0);
-      if (mbits) {
-        m0 = mbits[r * cpr + chunk];
-        m1 = mbits[(r + rpi) * cpr + chunk];
-      } else {
-        z0.load(zmask + r * C + c0);
-        z1.load(zmask + (r + rpi) * C + c0);
+    for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+      Vec8<T> g[U], z[U], av[U], bv[U];
+      uint32_t mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + (long)u * rpi;
+        g[u].load(dz + rr * C + c0);
+        mb[u] = 0;
+        if (mbits) mb[u] = mbits[rr * cpr + chunk];
+        else z[u].load(zmask + rr * C + c0);
+        av[u].load(ya + rr * C + c0);
+        bv[u].load(yb + rr * C + c0);
       }
-      a0.load(ya + r * C + c0);
-      a1.load(ya + (r + rpi) * C + c0);
-      b0.load(yb + r * C + c0);
-      b1.load(yb + (r + rpi) * C + c0);
-      acc(g0, z0, m0, a0, b0);
-      acc(g1, z1, m1, a1, b1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc(g[u], z[u], mb[u], av[u], bv[u]);
     }
-    if (r < r1) {
+    for (; r < r1; r += rpi) {
       Vec8<T> g0, z0, a0, b0;
       uint32_t m0 = 0;
       g0.load(dz + r * C + c0);

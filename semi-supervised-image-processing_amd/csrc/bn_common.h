@@ -149,28 +149,26 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
     }
   };
   if (rsub < rpi) {
-    // two rows in flight per thread; rows accumulate in the same order as a
-    // plain r += rpi walk, so the sums do not depend on the unroll
+    // four rows in flight per thread (one memory round trip covers a small
+    // tensor's whole share); rows accumulate in the same order as a plain
+    // r += rpi walk, so the sums do not depend on the unroll
+    constexpr int U = 4;
     long r = r0 + rsub;
-    for (; r + rpi < r1; r += 2 * rpi) {
-      Vec8<T> g0, g1, z0, z1, y0, y1;
-      uint32_t m0 = 0xFFu, m1 = 0xFFu;
-      g0.load(dz + r * C + c0);
-      g1.load(dz + (r + rpi) * C + c0);
-      y0.load(y + r * C + c0);
-      y1.load(y + (r + rpi) * C + c0);
-      if (zmask) {
-        z0.load(zmask + r * C + c0);
-        z1.load(zmask + (r + rpi) * C + c0);
+    for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+      Vec8<T> g[U], z[U], yv[U];
+      uint32_t mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + (long)u * rpi;
+        g[u].load(dz + rr * C + c0);
+        yv[u].load(y + rr * C + c0);
+        if (zmask) z[u].load(zmask + rr * C + c0);
+        mb[u] = mbits ? (uint32_t)mbits[rr * cpr + chunk] : 0xFFu;
       }
-      if (mbits) {
-        m0 = mbits[r * cpr + chunk];
-        m1 = mbits[(r + rpi) * cpr + chunk];
-      }
-      acc(g0, z0, m0, y0);
-      acc(g1, z1, m1, y1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc(g[u], z[u], mb[u], yv[u]);
     }
-    if (r < r1) {
+    for (; r < r1; r += rpi) {
       Vec8<T> g0, z0, y0;
       uint32_t m0 = 0xFFu;
       g0.load(dz + r * C + c0);
@@ -200,10 +198,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
 }
 
 static inline int bwd_rows_per_block(long M, int C) {
-  // aim for ~2048 blocks (8 per CU), at least four full iterations of rows
+  // aim for ~512 blocks (2 per CU), at least eight iterations of rows (fewer,
+  // longer blocks: 38.1 vs 43.8 us at layer1 batch 256, 15.6 vs 19.5 at layer3,
+  // tools/time_bn_bwd.py)
+  // (SSIP_BWD_BLOCKS / SSIP_BWD_ITERS: tuning overrides)
+  static const long nb = getenv("SSIP_BWD_BLOCKS") ? atol(getenv("SSIP_BWD_BLOCKS")) : 512;
+  static const long it = getenv("SSIP_BWD_ITERS") ? atol(getenv("SSIP_BWD_ITERS")) : 8;
   const int rpi = 256 / (C / 8);
-  long rows = (M + 2047) / 2048;
-  if (rows < 4 * rpi) rows = 4 * rpi;
+  long rows = (M + nb - 1) / nb;
+  if (rows < it * rpi) rows = it * rpi;
   if (rows < rpi) rows = rpi;
   rows = ((rows + rpi - 1) / rpi) * rpi;
   return (int)rows;

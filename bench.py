@@ -212,7 +212,14 @@ def main():
         elapsed = float(t.item())
     loss = out.loss.cpu().tolist()
 
-    # roofline leg: one instrumented step, HIP events around every conv launch
+    # roofline leg: one instrumented step, HIP events around every conv launch.
+    # Two more (unsynchronised) steps are queued first so the host enqueues
+    # the eager instrumented step while the device is still busy: each event
+    # bracket then holds its kernel's execution, not device idle time waiting
+    # for the host's next launch (the brackets agree with rocprofv3's kernel
+    # durations, profiles/r2_bench_family_summary.txt)
+    for _ in range(2):
+        step(x_l, y_l, x_u)
     timer = ops.ConvTimer()
     ops.set_conv_timer(timer)
     # the same kernels launched one by one from Python, each bracketed by events

@@ -93,12 +93,22 @@ struct WprepTable {
   ssip_wprep it[SSIP_WPREP_MAX];
   int tile_start[SSIP_WPREP_MAX + 1];
   int count;
+  int xcd;
 };
 
 template <typename T>
 __global__ void __launch_bounds__(256) weight_prep_batch_kernel(const WprepTable tab) {
   __shared__ float tile[64][65];
+  // XCD-aware order: the hardware deals workgroups round-robin to the 8 XCDs;
+  // remap so each XCD runs a contiguous range, which puts the R*Sp tap slices
+  // of one 64x64 (k, c) tile on one XCD: they read the same KCRS cache lines
+  // (a 36-B lane stride), fetched into that XCD's L2 once instead of by up
+  // to nine XCDs.  SSIP_WPREP_NO_XCD=1 (kernel arg xcd = 0) keeps the plain order.
   int b = blockIdx.x, idx = 0;
+  if (tab.xcd) {
+    const int nb = gridDim.x, xcd = b & 7, q = nb >> 3, r = nb & 7;
+    b = xcd * q + min(xcd, r) + (b >> 3);
+  }
   while (idx + 1 < tab.count && b >= tab.tile_start[idx + 1]) ++idx;
   const ssip_wprep& e = tab.it[idx];
   b -= tab.tile_start[idx];
@@ -207,6 +217,10 @@ extern "C" int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* it
     tiles += ((e.K + 63) / 64) * ((e.Cp + 63) / 64) * e.R * e.Sp;
   }
   tab.tile_start[count] = tiles;
+  {
+    static const bool no_xcd = getenv("SSIP_WPREP_NO_XCD") && getenv("SSIP_WPREP_NO_XCD")[0] == '1';
+    tab.xcd = no_xcd ? 0 : 1;
+  }
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(weight_prep_batch_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, tab);
   });

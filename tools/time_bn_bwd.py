@@ -52,7 +52,7 @@ def report(path):
         for k, v in by.items():
             us = sorted(v)[len(v) // 2]
             nbytes = 2 * t + M * C / 8 if "reduce" in k else (3 * t + M * C / 8 if "apply" in k else 0)
-            bw = f"{nbytes / us / 1e3:6.2f} TB/s" if nbytes else ""
+            bw = f"{nbytes / us / 1e6:6.2f} TB/s" if nbytes else ""
             print(f"{nm} M={M:7d} C={C:3d}  {k[:40]:40s} {us:7.1f} us  {bw}")
 
 

@@ -59,16 +59,20 @@ __global__ void augment_kernel(int B, const uint8_t* __restrict__ src, long src_
                                int Hr, int Wr, int Ho, int Wo, int cx, int cy, int ksize_v,
                                const int* __restrict__ bounds_v, const int* __restrict__ coeffs_v,
                                const ssip_aug_param* __restrict__ params, float m0, float m1, float m2, float s0,
-                               float s1, float s2, int opad, T* __restrict__ out) {
-  // one workgroup per output row (grid Hp x B): sample index and row are
-  // workgroup-uniform (the sample's parameters are scalar loads), no 64-bit
-  // index division per pixel
+                               float s1, float s2, int opad, int rows, T* __restrict__ out) {
+  // `rows` output rows per workgroup (grid ceil(Hp / rows) x B): sample index
+  // and row are workgroup-uniform (the sample's parameters are scalar loads),
+  // no 64-bit index division per pixel; several rows per workgroup amortise
+  // the wave launch over more than one pixel per thread
   const int Hp = Ho + 2 * opad, Wp = Wo + 2 * opad;
-  const int y = (int)blockIdx.x - opad;
   const int b = (int)blockIdx.y;
   const ssip_aug_param pa = params ? params[b] : ssip_aug_param{};
+  const int yp0 = (int)blockIdx.x * rows;
+  const int yp1 = min(Hp, yp0 + rows);
+  for (int yp = yp0; yp < yp1; ++yp)
   for (int xp = threadIdx.x; xp < Wp; xp += blockDim.x) {
-    const long i = ((long)b * Hp + blockIdx.x) * Wp + xp;
+    const int y = yp - opad;
+    const long i = ((long)b * Hp + yp) * Wp + xp;
     const int x = xp - opad;
     if (x < 0 || x >= Wo || y < 0 || y >= Ho) {  // zero border of a pre-padded stem input
       Vec4Px<T> z;
@@ -185,13 +189,16 @@ int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stri
   SSIP_REQUIRE(out_pad >= 0 && out_pad <= 8, SSIP_ERR_ARG, "ssip_augment_u8: out_pad must be 0..8");
   SSIP_REQUIRE((long)B * (Ho + 2 * out_pad) < 65536l * 65536l && B < 65536, SSIP_ERR_ARG,
                "ssip_augment_u8: batch too large");
-  const int wp = Wo + 2 * out_pad;
-  const dim3 grid((unsigned)(Ho + 2 * out_pad), (unsigned)B);
+  const int wp = Wo + 2 * out_pad, hp = Ho + 2 * out_pad;
+  // 4 rows per workgroup (SSIP_AUG_ROWS: tuning override)
+  static const int rows = getenv("SSIP_AUG_ROWS") ? std::max(1, atoi(getenv("SSIP_AUG_ROWS"))) : 4;
+  const dim3 grid((unsigned)((hp + rows - 1) / rows), (unsigned)B);
   const dim3 block((unsigned)(wp >= 256 ? 256 : ((wp + 63) / 64) * 64));
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(augment_kernel<T>, grid, block, 0, (hipStream_t)stream, B, src,
                        (long)src_batch_stride, src_h, src_w, Hr, Wr, Ho, Wo, crop_x, crop_y, ksize_v, bounds_v,
-                       coeffs_v, params, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], out_pad, (T*)out);
+                       coeffs_v, params, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], out_pad, rows,
+                       (T*)out);
   });
   return ::ssip::check_launch("augment_u8");
 }

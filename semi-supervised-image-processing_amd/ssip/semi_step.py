@@ -206,8 +206,10 @@ class SemiStep:
 
     def _optimizer_step(self, scale: float) -> None:
         """AdamW; with the stem wgrad still running on the side stream
-        (defer_stem_wgrad_join) every other parameter is updated and its
-        compute-dtype copies refreshed first, beside it, then conv1."""
+        (defer_stem_wgrad_join) every other parameter is enqueued first, with
+        no join on the side stream, then conv1.  (On MI355X the stem wgrad
+        holds every SIMD's register file, so the first update is dispatched
+        as it drains rather than beside it: profiles/r2_step_streams.txt.)"""
         m = self.model
         pend = m.take_pending_side()
         if pend is None:

@@ -323,6 +323,7 @@ def compute_accuracy_f1(y_true: Sequence[int], y_pred: Sequence[int]) -> Tuple[f
 def evaluate_on_loader(model: nn.Module, data_loader: DataLoader, criterion: nn.Module,
                        device: torch.device) -> Tuple[float, float, float]:
     model.eval()
+    D.sync_buffers(model)  # under DP: every shard evaluated with rank 0's running statistics
     losses: List[torch.Tensor] = []
     y_true: List[torch.Tensor] = []
     y_pred: List[torch.Tensor] = []
@@ -372,6 +373,9 @@ def train_model(model: nn.Module, train_loader: DataLoader, val_loader: DataLoad
             losses.append(loss.detach().view(1))
             yt.append(labels)
             yp.append(outputs.detach().argmax(dim=1))
+        # under DP: rank 0's BN running statistics on every rank (DDP's buffer
+        # broadcast) before the sharded validation pass and the checkpoint
+        D.sync_buffers(model)
         # under DP the epoch's metrics cover every rank's steps (gathered in rank order)
         sl = D.gather_list(torch.cat(losses).cpu().numpy().astype(np.float64).tolist() if losses else [])
         tl = float(np.mean(sl)) if sl else 0.0
@@ -421,6 +425,7 @@ def make_optimizer(model: SSIPResNet, lr: float, weight_decay: float, params=Non
 def evaluate_model(model: nn.Module, data_loader: DataLoader, device: torch.device, pos_index: Optional[int] = None,
                    threshold: Optional[float] = None):
     model.eval()
+    D.sync_buffers(model)
     y_true: List[int] = []
     y_pred: List[int] = []
     y_prob: List[float] = []

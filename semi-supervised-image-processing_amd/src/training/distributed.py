@@ -58,9 +58,11 @@ def is_main() -> bool:
     return rank() == 0
 
 
-def shard_loader(loader: DataLoader) -> DataLoader:
+def shard_loader(loader: DataLoader, even: bool = False) -> DataLoader:
     """This rank's contiguous run of the loader's batches (same batch size,
-    collate and workers; sequential loaders only)."""
+    collate and workers; sequential loaders only).  even=True (training: every
+    batch is a step with gradient all-reduces, so every rank must run the same
+    number) keeps only the first world * floor(nb / world) batches."""
     w = world()
     if w == 1:
         return loader
@@ -69,6 +71,8 @@ def shard_loader(loader: DataLoader) -> DataLoader:
     ds = loader.dataset
     n, bs = len(ds), loader.batch_size
     nb = math.ceil(n / bs) if not loader.drop_last else n // bs
+    if even:
+        nb -= nb % w
     blo, bhi = shard_range(nb, rank(), w)
     idx = list(range(blo * bs, min(bhi * bs, n)))
     return DataLoader(Subset(ds, idx), batch_size=bs, shuffle=False, num_workers=loader.num_workers,
@@ -83,7 +87,10 @@ def gather_list(local: list) -> list:
 class RankStridedSampler(Sampler):
     """The base sampler's stream, drawn identically on every rank (it consumes
     the global torch RNG like the reference's WeightedRandomSampler does at each
-    epoch's iter), rank-strided: rank r trains on draws r, r + world, ..."""
+    epoch's iter), padded to a multiple of world by repeating its head (as
+    torch's DistributedSampler pads) and rank-strided: rank r trains on draws
+    r, r + world, ...  Every rank gets ceil(n / world) draws, so every rank runs
+    the same number of batches (each one a step with gradient all-reduces)."""
 
     def __init__(self, base: Sampler, rank_: Optional[int] = None, world_: Optional[int] = None):
         self.base = base
@@ -91,11 +98,18 @@ class RankStridedSampler(Sampler):
         self.w = world() if world_ is None else world_
 
     def __iter__(self) -> Iterator[int]:
-        return iter(list(self.base)[self.r::self.w])
+        draws = list(self.base)
+        n = len(draws)
+        if n == 0:
+            return iter([])
+        total = -(-n // self.w) * self.w
+        while len(draws) < total:
+            draws += draws[: total - len(draws)]
+        return iter(draws[self.r::self.w])
 
     def __len__(self) -> int:
         n = len(self.base)
-        return (n - self.r + self.w - 1) // self.w if n > self.r else 0
+        return -(-n // self.w) if n > 0 else 0
 
 
 def broadcast_model(model) -> None:
@@ -104,8 +118,33 @@ def broadcast_model(model) -> None:
         return
     arena = model.flatten_parameters()
     dist.broadcast(arena.flat, 0)
-    for b in model.buffers():
-        dist.broadcast(b, 0)
+    sync_buffers(model)
+
+
+def sync_buffers(model) -> None:
+    """Rank 0's BatchNorm buffers (running_mean / running_var /
+    num_batches_tracked) on every rank, in one broadcast per dtype.
+
+    Training updates each rank's running statistics from its own batches
+    (DDP: local batch statistics, no SyncBN), so they drift apart; DDP
+    re-broadcasts rank 0's buffers (broadcast_buffers=True) and the model the
+    pipelines save and report is rank 0's.  Every sharded forward-only pass
+    (evaluation, pseudo-labelling, triage) therefore runs after this, so each
+    shard is computed with the statistics of that one model (reference: one
+    model evaluated in common.py:317-342,439-506; semi_supervised.py:44-72)."""
+    if world() == 1:
+        return
+    bufs = [b for b in model.buffers()]
+    for dt in sorted({b.dtype for b in bufs}, key=str):
+        group = [b for b in bufs if b.dtype == dt]
+        flat = torch.cat([b.reshape(-1) for b in group])
+        dist.broadcast(flat, 0)
+        o = 0
+        with torch.no_grad():
+            for b in group:
+                n = b.numel()
+                b.copy_(flat[o:o + n].view_as(b))
+                o += n
 
 
 def attach_grad_allreduce(model, optimizer) -> None:

@@ -57,6 +57,7 @@ def generate_pseudo_labels(model: nn.Module, data_loader: DataLoader, device: to
     (reference semi_supervised.py:44-72); softmax/max/threshold in one kernel,
     one device->host copy per batch."""
     model.eval()
+    D.sync_buffers(model)  # under DP: every shard labelled by rank 0's model
     out: List[Tuple[str, int, float]] = []
     with torch.no_grad():
         for images, paths in D.shard_loader(data_loader):
@@ -180,8 +181,10 @@ def train_consistency(model, base, train_idx, pool, val_loader, criterion, devic
     for epoch in range(config.weak_pretrain_epochs):
         model.train()
         order = torch.randperm(len(unl), generator=gen).tolist()
+        # every rank runs the same number of steps (each step all-reduces gradients)
         unl_loader = D.shard_loader(DataLoader(torch.utils.data.Subset(unl, order), batch_size=bs, shuffle=False,
-                                               num_workers=config.num_workers, collate_fn=_stack, drop_last=True))
+                                               num_workers=config.num_workers, collate_fn=_stack, drop_last=True),
+                                    even=True)
         lab_iter = iter(lab_loader)
         losses, yt, yp = [], [], []
         for xu, _ in unl_loader:
@@ -194,6 +197,7 @@ def train_consistency(model, base, train_idx, pool, val_loader, criterion, devic
             losses.append(out.loss[0:1].clone())
             yt.append(yl)
             yp.append(step.last["logits"][: yl.shape[0]].argmax(1).cpu())
+        D.sync_buffers(model)  # rank 0's running statistics before the sharded validation pass
         sl = D.gather_list(torch.cat(losses).cpu().double().tolist() if losses else [])
         tl = float(np.mean(sl)) if sl else 0.0
         ta, tf1 = compute_accuracy_f1(D.gather_list(torch.cat(yt).tolist() if yt else []),
@@ -345,6 +349,7 @@ def run_pipeline(config: TrainingConfig) -> Dict[str, Dict[str, float]]:
                                     num_workers=config.num_workers, pin_memory=torch.cuda.is_available(),
                                     collate_fn=Collate(tfm["eval"]))
             semi.eval()
+            D.sync_buffers(semi)
             recs = []
             with torch.no_grad():
                 for images, paths in D.shard_loader(tri_loader):

@@ -38,6 +38,19 @@ class ParamArena:
                 self.offsets[id(p)] = (off, n)
                 off += n
         self.numel = total
+        # a side stream still writing into ``grad`` (the deferred stem wgrad of
+        # SSIPResNet's backward); every consumer of the gradients or of the
+        # parameters joins it first (join_pending)
+        self.pending_side = None
+
+    def join_pending(self) -> None:
+        """Make the current stream wait for a side stream the last backward
+        left unjoined, and forget it."""
+        s, self.pending_side = self.pending_side, None
+        if s is not None:
+            from . import ops
+
+            ops.wait_stream(torch.cuda.current_stream(s.device), s)
 
     def owns(self, p: torch.Tensor) -> bool:
         ent = self.offsets.get(id(p))

@@ -34,6 +34,8 @@ class AdamW(torch.optim.Optimizer):
         self.dp_bucketer = None
 
     def zero_grad(self, set_to_none: bool = True) -> None:
+        if self.arena is not None:
+            self.arena.join_pending()  # a deferred stem wgrad may still write the arena's grads
         super().zero_grad(set_to_none=set_to_none)
         if self.dp_bucketer is not None:
             self.dp_bucketer.reset()
@@ -85,11 +87,16 @@ class AdamW(torch.optim.Optimizer):
         return runs, loose
 
     @torch.no_grad()
-    def step(self, closure=None, grad_scale: float = 1.0, only=None, skip=None, sched_step: bool = True):
+    def step(self, closure=None, grad_scale: float = 1.0, only=None, skip=None, sched_step: bool = True,
+             join_pending: bool = True):
         """One AdamW update.  ``only`` / ``skip``: sets of id(param) restricting
         the update to a subset (a step split around a pending gradient, see
         SemiStep); the later parts of a split pass ``sched_step=False`` so the
-        device schedule advances once per step."""
+        device schedule advances once per step.  Any gradient a side stream is
+        still writing (a deferred stem wgrad) is joined first unless the caller
+        updates only the other parameters (``join_pending=False``)."""
+        if join_pending and self.arena is not None:
+            self.arena.join_pending()
         loss = None
         if closure is not None:
             with torch.enable_grad():

@@ -260,7 +260,15 @@ class SSIPResNet(nn.Module):
         """The side stream whose stem wgrad the last backward left unjoined
         (defer_stem_wgrad_join), or None; clears it."""
         s, self._pending_side = self._pending_side, None
+        if self._arena is not None and self._arena.pending_side is s:
+            self._arena.pending_side = None
         return s
+
+    def join_pending_side(self) -> None:
+        """The current stream waits for a stem wgrad left unjoined (no-op otherwise)."""
+        s = self.take_pending_side()
+        if s is not None:
+            ops.wait_stream(torch.cuda.current_stream(s.device), s)
 
     def prepare_weights(self, need_t: bool = True, force: bool = False) -> None:
         """Refresh the compute-dtype conv weight copies now (one launch) so a
@@ -271,6 +279,8 @@ class SSIPResNet(nn.Module):
 
     # ------------------------------------------------------------------
     def forward(self, x):
+        # a previous backward's deferred stem wgrad still writes conv1's grad
+        self.join_pending_side()
         if isinstance(x, DeviceImages):
             images, pad = x.buf, x.pad
             if pad not in (0, self.conv1.padding[0]):
@@ -593,6 +603,8 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     finally:
         if deferred:
             model._pending_side = side
+            if model._arena is not None:
+                model._arena.pending_side = side  # AdamW.step / zero_grad join it
         else:
             ops.wait_stream(main, side)
 
@@ -852,7 +864,10 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                 ops.wait_stream(main, side)
             with torch.cuda.stream(side):
                 ops.stem_bwd_wgrad(*args)
-            for t in (dz, coef1):
+            # every tensor the side-stream kernel reads or writes was allocated
+            # on main: keep the caching allocator from handing any of them to a
+            # main-stream allocation before the join (deferred: after this returns)
+            for t in (dz, sv.pool_idx, stem.y, stem.x, stem.stats, coef1, workspace):
                 t.record_stream(side)
     else:
         defer = False

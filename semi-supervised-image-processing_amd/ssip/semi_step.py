@@ -35,7 +35,9 @@ from .resnet import DeviceImages, SSIPResNet
 
 @dataclass
 class StepStats:
-    loss: torch.Tensor        # [4] total, L_l, L_u, mask count (device)
+    # [4] total, L_l, L_u, mask count (device).  In plan mode every replay
+    # writes the same buffer: clone it to keep a step's value past the next step.
+    loss: torch.Tensor
 
 
 def _common_base(params):
@@ -95,7 +97,9 @@ class SemiStep:
         # single process, no graph capture: the optimizer overlaps the stem
         # wgrad at the end of the backward (a graph capture needs every forked
         # stream joined; a gradient bucketer reduces conv1's gradient itself)
-        model.defer_stem_wgrad_join = bucketer is None and not graph and os.environ.get("SSIP_DEFER_STEM") != "0"
+        # (scoped to this step's own backward: _fwd_bwd sets the model flag and
+        # clears it, so another trainer of the same model never defers)
+        self._defer = bucketer is None and not graph and os.environ.get("SSIP_DEFER_STEM") != "0"
 
     def _side_stream(self, dev):
         if self._side is None:
@@ -170,7 +174,11 @@ class SemiStep:
         if side is not main:
             ops.wait_stream(main, side)
             zw.record_stream(main)
-        return self._loss_bwd(logits, y_l, zw)
+        m.defer_stem_wgrad_join = self._defer
+        try:
+            return self._loss_bwd(logits, y_l, zw)
+        finally:
+            m.defer_stem_wgrad_join = False
 
     def __call__(self, x_l: torch.Tensor, y_l: torch.Tensor, x_u: torch.Tensor, params=None) -> StepStats:
         """x_l [Bl,H,W,3] u8, y_l [Bl] int64, x_u [Bu,H,W,3] u8 — all on the device."""
@@ -183,6 +191,10 @@ class SemiStep:
             return self._replay(x_l, y_l, x_u, params)
         if self.plan and self._calls > self.eager_warmup:
             return self._plan_step(x_l, y_l, x_u, params)
+        return self._eager_step(x_l, y_l, x_u, params)
+
+    def _eager_step(self, x_l, y_l, x_u, params) -> StepStats:
+        dev = x_l.device
         pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
         out = self._fwd_bwd(x_l, y_l, x_u, pl, pw, ps)
         scale = self.bucketer.finish() if self.bucketer is not None else 1.0
@@ -216,7 +228,7 @@ class SemiStep:
             self.opt.step(grad_scale=scale)
             return
         late = {id(m.conv1.weight)}
-        self.opt.step(grad_scale=scale, skip=late)
+        self.opt.step(grad_scale=scale, skip=late, join_pending=False)
         ops.wait_stream(torch.cuda.current_stream(), pend)
         self.opt.step(grad_scale=scale, only=late, sched_step=False)
 
@@ -246,6 +258,12 @@ class SemiStep:
                 self._optimizer_step(scale)
             self._plan, self._plan_out = plan, out
             return StepStats(loss=out)
+        # the plan replays fixed buffers: a batch of another shape (a short last
+        # batch) or dtype runs as an eager step instead
+        rec = self._static
+        if any(a.shape != b.shape or a.dtype != b.dtype
+               for a, b in zip((x_l, y_l, x_u) + tuple(params), rec)) or len(params) != len(rec) - 3:
+            return self._eager_step(x_l, y_l, x_u, params)
         for dst, src in zip(self._static[:3], (x_l, y_l, x_u)):
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src, non_blocking=True)

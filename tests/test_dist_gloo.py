@@ -122,11 +122,38 @@ def _pipeline_worker(rank, world, port, q):
         torch.manual_seed(5)
         s = D.RankStridedSampler(WeightedRandomSampler(w, num_samples=7, replacement=True))
         local = list(s)
-        ok &= local == glob[rank::world] and len(s) == len(local)
+        # padded to a multiple of world by repeating the head (DistributedSampler)
+        padded = glob + glob[: (-len(glob)) % world]
+        ok &= local == padded[rank::world] and len(s) == len(local) == 4
         parts = D.gather_list([local])
-        inter = [x for t in zip(*[p + [None] * (len(parts[0]) - len(p)) for p in parts]) for x in t if x is not None]
-        ok &= inter == glob
+        inter = [x for t in zip(*parts) for x in t]
+        ok &= inter == padded
         ok &= D.rank_sum([1.0, float(rank)]) == [float(world), float(sum(range(world)))]
+        # every rank runs the same number of training batches (each one a step
+        # with gradient all-reduces) whatever n % world and n % bs are
+        for n, bs in ((7, 2), (9, 4), (5, 3), (13, 3)):
+            torch.manual_seed(n)
+            smp = D.RankStridedSampler(WeightedRandomSampler([1.0] * n, num_samples=n, replacement=True))
+            nbat = len(list(DataLoader(list(range(n)), batch_size=bs, sampler=smp)))
+            ok &= len(set(D.gather_list([nbat]))) == 1
+            even = D.shard_loader(DataLoader(list(range(n)), batch_size=bs, shuffle=False, drop_last=True), even=True)
+            counts = D.gather_list([len(list(even))])
+            ok &= len(set(counts)) == 1 and counts[0] == (n // bs) // world
+        # rank 0's BN buffers on every rank, bitwise
+        bn = torch.nn.Sequential(torch.nn.BatchNorm2d(5), torch.nn.BatchNorm2d(3))
+        bn.train()
+        torch.manual_seed(100 + rank)
+        bn[0](torch.randn(4, 5, 2, 2) * (rank + 1))
+        bn[1](torch.randn(4, 3, 2, 2))
+        bn[0].num_batches_tracked += rank
+        mine0 = [b.clone() for b in bn.buffers()]
+        D.sync_buffers(bn)
+        got = D.gather_list([[b.tolist() for b in bn.buffers()]])
+        ok &= all(g == got[0] for g in got)
+        if rank == 0:
+            ok &= all(torch.equal(a, b) for a, b in zip(mine0, bn.buffers()))
+        else:
+            ok &= not all(torch.equal(a, b) for a, b in zip(mine0, bn.buffers()))
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()

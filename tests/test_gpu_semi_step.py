@@ -246,3 +246,72 @@ def test_semi_step_bf16_224_matches_oracle(dev):
             assert e_g <= max(3 * e_e, 1e-3 * b.abs().max().item()), k
         else:
             assert torch.equal(bufs_gpu[k], b.cpu()), k
+
+
+def _finetune_after_semi(dev, defer_env, monkeypatch):
+    """SemiStep steps (single process, stem wgrad deferral as configured), then
+    a plain train_model-style fine-tune of the SAME model with a fresh AdamW."""
+    from ssip.augment import draw_params_batch
+    from ssip.optim import AdamW
+
+    monkeypatch.setenv("SSIP_DEFER_STEM", defer_env)
+    S, B = 64, 8
+    torch.manual_seed(0)
+    m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2).to(dev).train()
+    step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=S, seed=0)
+    g = torch.Generator().manual_seed(3)
+    x_l = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    x_u = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    y_l = torch.randint(0, 2, (B,), generator=g).to(dev)
+    for _ in range(2):
+        step(x_l, y_l, x_u, (draw_params_batch(B, S, False, g), draw_params_batch(B, S, False, g),
+                             draw_params_batch(B, S, True, g)))
+    # the deferral is scoped to SemiStep's own backward
+    assert m.defer_stem_wgrad_join is False and m._pending_side is None and step.arena.pending_side is None
+    opt = AdamW([p for p in m.parameters()], lr=5e-5, weight_decay=1e-4, arena=m.flatten_parameters())
+    xf = torch.randn(B, 3, S, S, generator=g).to(dev)
+    yf = torch.randint(0, 2, (B,), generator=g).to(dev)
+    for _ in range(3):
+        opt.zero_grad()
+        out = m(xf)
+        torch.nn.functional.cross_entropy(out, yf).backward()
+        assert m._pending_side is None  # a plain backward joins its stem wgrad
+        opt.step()
+    torch.cuda.synchronize()
+    return m.conv1.weight.detach().cpu().clone(), step.arena.flat.detach().cpu().clone()
+
+
+def test_train_after_semi_step_same_model(dev, monkeypatch):
+    """a SemiStep left defer_stem_wgrad_join set on the model, so a
+    later fine-tune's AdamW / zero_grad raced the stem wgrad still writing
+    conv1's gradient.  Deferred and non-deferred SemiSteps followed by the
+    same fine-tune must give bit-identical weights (conv1 included)."""
+    w_def, flat_def = _finetune_after_semi(dev, "1", monkeypatch)
+    w_ser, flat_ser = _finetune_after_semi(dev, "0", monkeypatch)
+    assert torch.equal(w_def, w_ser)
+    assert torch.equal(flat_def, flat_ser)
+
+
+def test_plan_step_shape_change_runs_eagerly(dev):
+    """a batch of another shape than the recorded plan's (a short last
+    batch) runs as an eager step instead of being copied into the plan's buffers."""
+    from ssip.augment import draw_params_batch
+
+    S, B = 64, 8
+    torch.manual_seed(0)
+    m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2).to(dev).train()
+    step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=S, seed=0, plan=True, eager_warmup=1)
+    g = torch.Generator().manual_seed(3)
+
+    def batch(b):
+        return (torch.randint(0, 256, (b, S, S, 3), generator=g, dtype=torch.uint8).to(dev),
+                torch.randint(0, 2, (b,), generator=g).to(dev),
+                torch.randint(0, 256, (b, S, S, 3), generator=g, dtype=torch.uint8).to(dev))
+
+    for b in (B, B, B, 5, B):  # eager warm-up, record, replay, short batch, replay
+        x_l, y_l, x_u = batch(b)
+        out = step(x_l, y_l, x_u)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out.loss).all()
+    assert step._plan is not None and step._static[0].shape[0] == B
+    assert step.opt.device_step_count() == 5

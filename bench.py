@@ -68,7 +68,28 @@ def parse():
                     help="semi: the north-star train step (default); extract: src.feature_extraction's frozen "
                          "ResNet-18 embedding pass (the reference's only published throughput, 358.6 images/s)")
     ap.add_argument("--extract-images", type=int, default=1506, help="images of the end-to-end extraction run")
+    ap.add_argument("--cpu-warmup", type=int, default=1,
+                    help="CPU-baseline warm-up steps (BASELINE.md section 3 asks >= 10: pass --cpu-warmup 10 "
+                         "--cpu-steps 50 for the full protocol, ~6-7 min on 16 host cores)")
+    ap.add_argument("--cpu-steps", type=int, default=4, help="CPU-baseline timed steps (median reported)")
     return ap.parse_args()
+
+
+def host_cores() -> dict:
+    """The host cores this process can actually run on: the affinity mask,
+    capped by a cgroup CPU quota when one is set (a GPU box's CPU share can be
+    a quota over a machine-wide affinity mask).  An inherited OMP_NUM_THREADS
+    does not cap it."""
+    avail = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    cores = avail if quota is None else max(1, min(avail, int(quota + 0.5)))
+    return {"cores": cores, "affinity": avail, "cgroup_quota": quota, "total": os.cpu_count()}
 
 
 def extract_bench(args):
@@ -259,13 +280,17 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.step_oracle import time_cpu_step
 
-        # the host cores this process may run on (the box's CPU share), capped by
-        # OMP_NUM_THREADS when set; the machine's total is reported beside it
-        avail = len(os.sched_getaffinity(0))
-        threads = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)))
-        c = time_cpu_step(Bl=Bl, Bu=Bu, steps=5, warmup=2, threads=threads)
+        # one thread per host core this process may use
+        hc = host_cores()
+        c = time_cpu_step(Bl=Bl, Bu=Bu, steps=args.cpu_steps, warmup=args.cpu_warmup, threads=hc["cores"])
+        full = args.cpu_warmup >= 10 and args.cpu_steps >= 50
         cpu = {"value": round(c["value"], 3), "unit": "images/s", "cores": c["threads"], "kind": "port",
-               "sample": c["sample"], "host_cpus_affinity": avail, "host_cpus_total": os.cpu_count(),
+               "threads": c["threads"], "host_cores": hc["cores"], "host_cpus_affinity": hc["affinity"],
+               "host_cgroup_quota": hc["cgroup_quota"], "host_cpus_total": hc["total"],
+               "sample": c["sample"] + ("" if full else
+                                        "; reduced from BASELINE.md section 3's >=10 warm-up + median of >=50 "
+                                        "timed steps to bound the bench's run time (full protocol: "
+                                        "--cpu-warmup 10 --cpu-steps 50)"),
                "step_times_s": [round(t, 3) for t in c["step_times_s"]]}
 
     if rank == 0:

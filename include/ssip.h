@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 7
+#define SSIP_ABI_VERSION 8
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -99,6 +99,19 @@ int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype);
 int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
                        const void* zmask, const void* y, const float* mean, const float* invstd, void* dpre,
                        float* partial, void* stream);
+/* Forward of a downsampling block's first conv (3x3, pad 1, stride s) and its
+ * 1x1 / stride-s downsample (torchvision BasicBlock conv1 + downsample[0],
+ * both `model(inputs)` at src/training/common.py:380) over the same input x:
+ * one launch (ABI 8) -- the downsample's GEMM is the conv's tap-(1,1) column
+ * block with W_ds [K][C] (KRSC of a 1x1 filter), so its short tiles run as
+ * extra workgroups of the conv's grid.  Outputs and BN partial records as two
+ * ssip_conv_fwd calls; the downsample's records per channel are
+ * ssip_conv_fwd_ds_partial_tiles(d, dds, dtype) (both buffers sized by
+ * ssip_conv_fwd_partial_floats of their own descriptor).  Falls back to two
+ * launches where the conv does not take the LDS-DMA ring kernel. */
+int ssip_conv_fwd_ds_partial_tiles(const ssip_conv_desc* d, const ssip_conv_desc* dds, int dtype);
+int ssip_conv_fwd_ds(const ssip_conv_desc* d, const ssip_conv_desc* dds, int dtype, const void* x, const void* w_krsc,
+                     void* y, float* bn_partial, const void* wds_kc, void* y_ds, float* bn_partial_ds, void* stream);
 /* Eval-mode conv + folded BatchNorm (+ residual) (+ ReLU), one launch:
  *   y = act(conv(x, w') + bias[k] (+ residual)),  w' = w * scale[k] (ssip_wprep.kscale)
  * (torchvision BasicBlock / Bottleneck in eval mode: bn(conv(x)) with running
@@ -259,13 +272,17 @@ int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, int out_pad
 int ssip_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
                float beta2, float eps, float weight_decay, int64_t step, float grad_scale, void* stream);
 /* Graph-replayable AdamW (same update as ssip_adamw): the schedule lives on the
- * device, sched = {lr, t, lr / (1 - beta1^t), sqrt(1 - beta2^t)} (fp64).
+ * device, sched = {lr, t, lr / (1 - beta1^t), sqrt(1 - beta2^t), counter} (fp64;
+ * slot 4 is an arrival counter, zero between launches).
  * ssip_adamw_sched_step advances t and the bias corrections (one thread);
- * ssip_adamw_dev applies the update reading them, so no per-step host scalar
- * is baked into a captured hipGraph.  (torch.optim.AdamW, semi_supervised.py:115-122) */
+ * ssip_adamw_dev applies the update reading them -- or, with advance != 0,
+ * advances them itself (ABI 8: the first update launch of a step; no
+ * separate schedule launch) -- so no per-step host scalar is baked into a
+ * captured hipGraph or launch plan.  (torch.optim.AdamW, semi_supervised.py:115-122) */
 int ssip_adamw_sched_step(double* sched, float beta1, float beta2, void* stream);
-int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const double* sched,
-                   float beta1, float beta2, float eps, float weight_decay, float grad_scale, void* stream);
+int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, double* sched,
+                   float beta1, float beta2, float eps, float weight_decay, float grad_scale, int advance,
+                   void* stream);
 /* w_kcrs (fp32 torchvision layout) -> w_krsc [K][R][Sp][Cp] and/or w_crsk [Cp][R][Sp][K] in dtype */
 int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, const float* w_kcrs, void* w_krsc,
                      void* w_crsk, void* stream);

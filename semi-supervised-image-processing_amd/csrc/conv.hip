@@ -99,6 +99,17 @@ struct ConvArgs {
   uint32_t a2_bytes, b2_bytes;
   int ds_from;
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
+  // FWD of a 3x3 / stride-s conv fused with its block's 1x1 / stride-s
+  // downsample (ssip_conv_fwd_ds): workgroups >= fwd_tiles1 compute the
+  // downsample's tiles -- its input pixel is the conv's tap (1, 1) pixel, so
+  // they run only that tap's C/64 k-steps, with W_ds [K][C] as B -- into
+  // out_ds / partial_ds.  0: no downsample.
+  int fwd_tiles1;
+  const void* Bds;
+  void* out_ds;
+  float* partial_ds;
+  uint32_t bds_bytes;
+  int stat_tiles_m;  // BN record tiles per channel when the grid is not tiles_m x tiles_n (0: from the grid)
   uint32_t a_bytes, b_bytes;  // operand extents (LDS-DMA kernel buffer resources)
   // WGRAD x-gather walk: a 64-row k-step advances each row's output pixel
   // (n, p, q) by (dn, dp, dq); its input byte offset by k0, plus e1 when q
@@ -376,7 +387,8 @@ template <int MODE, typename T, int BM, int BN, int WMW, int WNW, int FM, int FN
           bool FOLD = false>
 __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&acc)[FM][FN], char* smem, int m0,
                                                    int n0, int tm, const BnPostRegs<T, BM, BN, 64 * WMW * WNW>& pre,
-                                                   bool pre_loaded, const RowMap& rmap, int split) {
+                                                   bool pre_loaded, const RowMap& rmap, int split,
+                                                   void* out_alt = nullptr, float* partial_alt = nullptr) {
   constexpr int NT = 64 * WMW * WNW;
   constexpr int WTM = BM / WMW, WTN = BN / WNW;
   const int tid = threadIdx.x;
@@ -438,7 +450,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
   {
     // each thread moves 8-element chunks: BN/8 chunks per row
     constexpr int CPR = BN / 8;
-    T* Out = static_cast<T*>(a.out);   // may alias Add (in-place residual-gradient add)
+    T* Out = static_cast<T*>(out_alt ? out_alt : a.out);   // may alias Add (in-place residual-gradient add)
     const T* Add = static_cast<const T*>(a.add);
     for (int id = tid; id < BM * CPR; id += NT) {
       const int row = id / CPR, ch = id % CPR;
@@ -480,7 +492,8 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
   }
 
   if constexpr (MODE == MODE_FWD) {
-    if (a.partial == nullptr) return;
+    float* const partial = partial_alt ? partial_alt : a.partial;
+    if (partial == nullptr) return;
     __syncthreads();
     // BatchNorm partial statistics over this tile's valid rows (from fp32 accumulators).
     float* red = reinterpret_cast<float*>(smem);  // [WMW][BN]
@@ -536,14 +549,14 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
       for (int j = 0; j < FN; ++j) red[wm * BN + cbase + j * 16] = q2[j];
     }
     __syncthreads();
-    const int tiles_m = gridDim.x / a.tiles_n;
+    const int tiles_m = a.stat_tiles_m > 0 ? a.stat_tiles_m : (int)(gridDim.x / a.tiles_n);
     for (int c = tid; c < BN; c += NT) {
       const int n = n0 + c;
       if (n < a.Ng) {
         float t = 0.f;
 #pragma unroll
         for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-        float* rec = a.partial + ((long)n * tiles_m + tm) * 3;  // [C][tiles][3]
+        float* rec = partial + ((long)n * tiles_m + tm) * 3;  // [C][tiles][3]
         rec[0] = (float)cnt;
         rec[1] = mean_t[c] * (float)cnt;
         rec[2] = t;
@@ -929,6 +942,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   // tiles (same split/phase, neighbouring M-tiles sharing im2col rows and the
   // whole weight panel) instead of every 8th tile.
   int bx, by;
+  bool ds = false;  // FWD: a fused downsample tile (ConvArgs::fwd_tiles1)
   {
     const int nb = gridDim.x * gridDim.y;
     const int lin = blockIdx.x + blockIdx.y * gridDim.x;
@@ -940,6 +954,16 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
     } else {
       bx = t % gridDim.x;
       by = t / gridDim.x;
+    }
+    if (MODE == MODE_FWD && a.fwd_tiles1 > 0) {
+      // fused downsample: the conv's tiles first in dispatch order, then the
+      // short downsample tiles (they fill the last round), each group remapped
+      // XCD-contiguously on its own
+      ds = lin >= a.fwd_tiles1;
+      const int base = ds ? a.fwd_tiles1 : 0, cnt = ds ? nb - a.fwd_tiles1 : a.fwd_tiles1;
+      const int l = lin - base, x8 = l & 7, q8 = cnt >> 3, r8 = cnt & 7;
+      bx = a.xcd_remap ? x8 * q8 + min(x8, r8) + (l >> 3) : l;
+      by = 0;
     }
   }
   const int tn = bx % a.tiles_n;
@@ -959,7 +983,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   rmap.phased = phased;
   rmap.H = a.H;
   rmap.W = a.W;
-  int ph_nr = a.R, ph_ns = a.S, ph_r0 = 0, ph_s0 = 0, ph_bh = 0, ph_bw = 0, ph_ksteps = a.ksteps;
+  int ph_nr = a.R, ph_ns = a.S, ph_r0 = 0, ph_s0 = 0, ph_bh = 0, ph_bw = 0,
+      ph_ksteps = (MODE == MODE_FWD && ds) ? a.C / 64 : a.ksteps;
   if (phased) {
     if (tm >= SSIP_PSEL(tiles_m)) return;
     // a phase no tap reaches (1x1 stride-2 dgrad: 3 of 4) adds nothing: with
@@ -998,6 +1023,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   int b_r[LB], b_s[LB], b_c[LB], b_row[LB];
   bool b_ok[LB];
   int kr = 0, ks_ = 0, kcb = 0;
+  if (MODE == MODE_FWD && ds) { kr = 1; ks_ = 1; }  // the downsample's pixel is the conv's tap (1, 1)
   const int Cred = (MODE == MODE_FWD) ? a.C : a.K;
   long mstart = 0, mend = 0;
 
@@ -1088,7 +1114,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   // taps (bit r*S + s) whose source pixel lies inside the image.
   constexpr bool BUF_A = !C4;
   uint32_t a_off[LA], a_msk[LA], b_off[LB];
-  __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ag, a.a_bytes), rsB = make_rsrc(Bg, a.b_bytes);
+  __amdgpu_buffer_rsrc_t rsA = make_rsrc(Ag, a.a_bytes),
+                         rsB = (MODE == MODE_FWD && ds) ? make_rsrc(a.Bds, a.bds_bytes) : make_rsrc(Bg, a.b_bytes);
+  const int b_stride = (MODE == MODE_FWD && ds) ? a.C : a.Kg;  // B row length (W_ds: [K][C])
   const bool dsx = (MODE == MODE_DGRAD) && phased && f == 0 && a.A2 != nullptr;
   if constexpr (!WG && BUF_A) {
     const int nr = phased ? ph_nr : a.R, ns = phased ? ph_ns : a.S;
@@ -1116,7 +1144,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
 #pragma unroll
     for (int t = 0; t < LB; ++t) {
       const int row = 8 * (wave + NW * t) + (lane >> 3);
-      b_off[t] = b_ok[t] ? (uint32_t)(((long)(n0 + row) * a.Kg + b_c[t] * 8) * 2) : 0xF0000000u;
+      b_off[t] = b_ok[t] ? (uint32_t)(((long)(n0 + row) * b_stride + b_c[t] * 8) * 2) : 0xF0000000u;
     }
   } else if constexpr (WG) {
 #pragma unroll
@@ -1571,8 +1599,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   if constexpr (MODE == MODE_DGRAD && POST)
     conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
   else
-    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN, false, FOLD>(a, acc, smem, m0, n0, tm, post, false, rmap,
-                                                                       by);
+    conv_epilogue_impl<MODE, T, BM, BN, WMW, WNW, FM, FN, false, FOLD>(
+        a, acc, smem, m0, n0, tm, post, false, rmap, by, (MODE == MODE_FWD && ds) ? a.out_ds : nullptr,
+        (MODE == MODE_FWD && ds) ? a.partial_ds : nullptr);
 }
 
 // WGRAD slab reduction:  dW[k][c][r][s] (torchvision KCRS, fp32) =
@@ -2732,9 +2761,11 @@ static void choose_glds(int mode, const ConvArgs& a, Plan& pl) {
   }
   pl.bm = 128; pl.wmw = 4; pl.wnw = 2;
   pl.bn = (a.Ng % 128 == 0) ? 128 : 64;
-  // 256x256 tiles (8 waves of 64x128) where a forward still has >= 160 of them
-  // (ResNet-18 layer3: 62.7 vs 69.1 us, profiles/r1_conv_tune.txt)
-  if (mode == MODE_FWD && a.Ng % 256 == 0 && (long)ceil_div(a.M, 256) * (a.Ng / 256) >= 160) {
+  // 256x256 tiles (8 waves of 64x128) where a forward or stride-1 dgrad still
+  // has >= 160 of them (ResNet-18 layer3: fwd 62.7 vs 69.1 us,
+  // profiles/r1_conv_tune.txt; dgrad 62.4 vs 67.8 us, profiles/r3_tune_fd.txt)
+  if ((mode == MODE_FWD || (mode == MODE_DGRAD && a.stride == 1)) && a.Ng % 256 == 0 &&
+      (long)ceil_div(a.M, 256) * (a.Ng / 256) >= 160) {
     pl.bm = 256; pl.bn = 256;
   } else if (mode == MODE_FWD && a.Ng % 128 == 0 && (long)ceil_div(a.M, 128) * (a.Ng / 128) <= device_cus()) {
     // at most one 128x128 tile per CU (the weak forward's layer4 at batch 128:
@@ -3264,6 +3295,51 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
   pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_FWD, T>(pl, (hipStream_t)stream));
+}
+
+// A 3x3 / pad-1 / stride-s conv and its block's 1x1 / pad-0 / stride-s
+// downsample over the same input and output grid: one LDS-DMA launch when the
+// conv takes a 2- or 3-stage ring kernel (else false: two launches).
+static bool fwd_ds_plan(const ssip_conv_desc* d, const ssip_conv_desc* dds, int dtype, Plan& pl) {
+  if (dtype != SSIP_BF16 || !desc_ok(d) || !desc_ok(dds) || getenv("SSIP_NO_FWD_DSFUSE")) return false;
+  if (d->R != 3 || d->S != 3 || d->pad != 1 || dds->R != 1 || dds->S != 1 || dds->pad != 0 ||
+      dds->stride != d->stride || dds->N != d->N || dds->H != d->H || dds->W != d->W || dds->C != d->C ||
+      dds->K != d->K || dds->P != d->P || dds->Q != d->Q || d->C % 64 != 0)
+    return false;
+  HaloPlan hp;
+  if (halo_plan(MODE_FWD, d, dtype, hp) || stem_plan(d, dtype, hp)) return false;
+  if (plan_conv(MODE_FWD, d, 2, pl) != SSIP_OK || pl.conv1) return false;
+  return pl.stages == 2 || pl.stages == 3;
+}
+
+int ssip_conv_fwd_ds_partial_tiles(const ssip_conv_desc* d, const ssip_conv_desc* dds, int dtype) {
+  Plan pl;
+  if (fwd_ds_plan(d, dds, dtype, pl)) return ceil_div(pl.args.M, pl.bm);
+  return ssip_conv_fwd_partial_tiles(dds, dtype);
+}
+
+int ssip_conv_fwd_ds(const ssip_conv_desc* d, const ssip_conv_desc* dds, int dtype, const void* x, const void* w_krsc,
+                     void* y, float* bn_partial, const void* wds_kc, void* y_ds, float* bn_partial_ds, void* stream) {
+  SSIP_REQUIRE(x && w_krsc && y && wds_kc && y_ds, SSIP_ERR_ARG, "ssip_conv_fwd_ds: null pointer");
+  Plan pl;
+  if (!fwd_ds_plan(d, dds, dtype, pl)) {  // two launches
+    int rc = ssip_conv_fwd(d, dtype, x, w_krsc, y, bn_partial, stream);
+    if (rc) return rc;
+    return ssip_conv_fwd(dds, dtype, x, wds_kc, y_ds, bn_partial_ds, stream);
+  }
+  SSIP_REQUIRE((bn_partial == nullptr) == (bn_partial_ds == nullptr), SSIP_ERR_ARG,
+               "ssip_conv_fwd_ds: both or neither BN partial buffers");
+  ConvArgs& a = pl.args;
+  a.A = x; a.B = w_krsc; a.out = y; a.partial = bn_partial;
+  a.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
+  a.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
+  const int T1 = (int)pl.grid.x;
+  a.fwd_tiles1 = T1;
+  a.Bds = wds_kc; a.out_ds = y_ds; a.partial_ds = bn_partial_ds;
+  a.bds_bytes = (uint32_t)((long)d->K * d->C * 2);
+  a.stat_tiles_m = ceil_div(a.M, pl.bm);
+  pl.grid = dim3(2 * T1, 1, 1);
+  return launch_conv<MODE_FWD, __bf16>(pl, (hipStream_t)stream);
 }
 
 int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {

@@ -43,12 +43,25 @@ __global__ void adamw_sched_kernel(double* sched, double b1, double b2) {
   sched[3] = sqrt(1.0 - pow(b2, t));
 }
 
+// advance != 0: this launch also advances the schedule (t + 1 and the bias
+// corrections, computed per workgroup from sched[0..1] exactly as
+// adamw_sched_kernel does), and the last workgroup to finish (an arrival
+// count in sched[4], left at zero) writes them back -- every workgroup has
+// read sched[1] by then.  Saves the one-thread schedule launch per step.
 __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                                 float* __restrict__ v, const double* __restrict__ sched, float b1, float b2,
-                                 float eps, float wd, float grad_scale) {
+                                 float* __restrict__ v, double* sched, float b1, float b2, float eps, float wd,
+                                 float grad_scale, int advance) {
+  // wave-uniform schedule values, no LDS: this launch shares the CUs with the
+  // stem wgrad, which holds all of their LDS (conv_stem_bwd_wgrad_kernel)
+  double t = sched[1], ss = sched[2], bc = sched[3];
+  if (advance) {
+    t += 1.0;
+    ss = sched[0] / (1.0 - pow((double)b1, t));
+    bc = sqrt(1.0 - pow((double)b2, t));
+  }
   const float lr = (float)sched[0];
-  const float step_size = (float)sched[2];
-  const float bc2_sqrt = (float)sched[3];
+  const float step_size = (float)ss;
+  const float bc2_sqrt = (float)bc;
   const float decay = 1.f - lr * wd;
   const float w1 = 1.f - b1;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -62,6 +75,16 @@ __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __r
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
+  }
+  if (advance && threadIdx.x == 0) {
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(sched + 4);
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      sched[1] = t;
+      sched[2] = ss;
+      sched[3] = bc;
+      __hip_atomic_store(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -171,15 +194,15 @@ int ssip_adamw_sched_step(double* sched, float beta1, float beta2, void* stream)
   return ::ssip::check_launch("adamw_sched");
 }
 
-int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                   const double* sched, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, double* sched,
+                   float beta1, float beta2, float eps, float weight_decay, float grad_scale, int advance,
                    void* stream) {
   SSIP_REQUIRE(n > 0 && param && grad && exp_avg && exp_avg_sq && sched, SSIP_ERR_ARG,
                "ssip_adamw_dev: bad arguments");
   long blocks = (n + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 2048) blocks = 2048;  // grid-stride: each wave computes the schedule scalars once
   hipLaunchKernelGGL(adamw_dev_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
-                     exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale);
+                     exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale, advance ? 1 : 0);
   return ::ssip::check_launch("adamw_dev");
 }
 

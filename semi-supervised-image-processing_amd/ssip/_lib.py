@@ -29,7 +29,7 @@ def abi_version_expected() -> int:
     return int(m.group(1)) if m else ABI_VERSION
 
 
-ABI_VERSION = 7  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
+ABI_VERSION = 8  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1
@@ -85,6 +85,8 @@ _SIGS = {
     "ssip_conv_fwd": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_conv_dgrad_ds": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ssip_conv_fwd_ds_partial_tiles": (_c_int, [_PD, _PD, _c_int]),
+    "ssip_conv_fwd_ds": (_c_int, [_PD, _PD, _c_int] + [_vp] * 8),
     "ssip_conv_fwd_bias": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "ssip_conv_dgrad_bn_partial_floats": (_c_i64, [_PD]),
     "ssip_conv_dgrad_bn_partial_tiles": (_c_int, [_PD, _c_int]),
@@ -123,7 +125,7 @@ _SIGS = {
     "ssip_nchw_to_nhwc": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp]),
     "ssip_adamw": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i64, _c_f, _vp]),
     "ssip_adamw_sched_step": (_c_int, [_vp, _c_f, _c_f, _vp]),
-    "ssip_adamw_dev": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _vp]),
+    "ssip_adamw_dev": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_f, _c_f, _c_f, _c_int, _vp]),
     "ssip_weight_prep": (_c_int, [_c_int] * 7 + [_vp, _vp, _vp, _vp]),
     "ssip_weight_prep_batch": (_c_int, [_c_int, _c_int, ctypes.POINTER(WPrep), _vp]),
     "ssip_counters_add": (_c_int, [_c_int, _vp, _c_i64, _vp]),
@@ -170,7 +172,7 @@ def check(rc: int, what: str) -> None:
 
 
 # int-returning queries (not status codes)
-_NOT_STATUS = ("ssip_version", "ssip_conv_fwd_partial_tiles", "ssip_conv_dgrad_bn_partial_tiles",
+_NOT_STATUS = ("ssip_version", "ssip_conv_fwd_partial_tiles", "ssip_conv_fwd_ds_partial_tiles", "ssip_conv_dgrad_bn_partial_tiles",
                "ssip_stem_bwd_wgrad_supported", "ssip_plan_fn_index", "ssip_plan_segments")
 
 # Active launch-plan recorder (ssip.plan.PlanRecorder) or None.  While set,

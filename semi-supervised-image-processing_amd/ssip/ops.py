@@ -196,6 +196,35 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor
     call("ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial), stream_ptr())
 
 
+def conv_fwd_ds_partial_tiles(g: ConvGeom, gds: ConvGeom, dtype: torch.dtype) -> int:
+    """BN records per channel the fused forward writes for the downsample."""
+    key = ("pds", g, gds, dtype, _plan_env(), os.environ.get("SSIP_NO_FWD_DSFUSE"))
+    t = _plan_cache.get(key)
+    if t is None:
+        t = int(_lib.lib().ssip_conv_fwd_ds_partial_tiles(g.desc(), gds.desc(), _DT[dtype]))
+        if t <= 0:
+            raise RuntimeError(_lib.lib().ssip_last_error().decode())
+        _plan_cache[key] = t
+    return t
+
+
+def conv_fwd_ds(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor, partial: Optional[torch.Tensor],
+                gds: ConvGeom, wds: torch.Tensor, y_ds: torch.Tensor, partial_ds: Optional[torch.Tensor]) -> None:
+    """A downsampling block's conv1 (3x3) and 1x1 downsample forwards over the
+    same x in one launch (ssip_conv_fwd_ds)."""
+    assert x.numel() == g.N * g.H * g.W * g.C and w_krsc.numel() == g.K * g.R * g.S * g.C, "conv_fwd_ds: shapes"
+    assert y.numel() == y_ds.numel() == g.N * g.P * g.Q * g.K and wds.numel() == g.K * g.C, "conv_fwd_ds: shapes"
+    assert x.dtype == w_krsc.dtype == y.dtype == wds.dtype == y_ds.dtype
+    if partial is not None:
+        assert partial.numel() >= conv_fwd_partial_floats(g) and partial_ds.numel() >= conv_fwd_partial_floats(gds)
+    args = ("ssip_conv_fwd_ds", g.desc(), gds.desc(), dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial),
+            _p(wds), _p(y_ds), _p(partial_ds), stream_ptr())
+    if _timer is not None:
+        _timer.wrap("fwd", g.flops() + gds.flops(), call, *args)
+        return
+    call(*args)
+
+
 def conv_fwd_bias(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, bias: torch.Tensor,
                   residual: Optional[torch.Tensor], relu: bool, y: torch.Tensor) -> None:
     """y = act(conv(x, w) + bias (+ residual)): eval-mode conv with its BN folded in (ssip_conv_fwd_bias)."""
@@ -504,13 +533,17 @@ def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
 
 
 def adamw_sched_step(sched: torch.Tensor, beta1: float, beta2: float) -> None:
-    assert sched.dtype == torch.float64 and sched.numel() == 4
+    assert sched.dtype == torch.float64 and sched.numel() >= 4
     call("ssip_adamw_sched_step", _p(sched), float(beta1), float(beta2), stream_ptr())
 
 
-def adamw_dev(param, grad, exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale=1.0) -> None:
+def adamw_dev(param, grad, exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale=1.0,
+              advance: bool = False) -> None:
+    """advance: this launch also advances the device schedule (t, bias
+    corrections) -- the first update launch of a step; sched needs 5 slots."""
+    assert sched.dtype == torch.float64 and sched.numel() >= (5 if advance else 4)
     call("ssip_adamw_dev", param.numel(), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(sched), float(beta1),
-         float(beta2), float(eps), float(weight_decay), float(grad_scale), stream_ptr())
+         float(beta2), float(eps), float(weight_decay), float(grad_scale), int(bool(advance)), stream_ptr())
 
 
 def nchw_to_nhwc(x: torch.Tensor, Cp: int, dtype: torch.dtype, pad: int = 0) -> torch.Tensor:

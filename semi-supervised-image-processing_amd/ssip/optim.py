@@ -41,8 +41,8 @@ class AdamW(torch.optim.Optimizer):
             self.dp_bucketer.reset()
 
     def use_device_schedule(self) -> None:
-        """Keep lr and the step count on the device (``ssip_adamw_sched_step``
-        + ``ssip_adamw_dev``): ``step()`` then enqueues kernels only — no host
+        """Keep lr and the step count on the device (``ssip_adamw_dev``, whose
+        first launch of a step advances them): ``step()`` then enqueues kernels only — no host
         scalar changes per step, so it can run inside a captured hipGraph.
         All parameters of a group advance together (torch keeps one count per
         parameter; they agree whenever every parameter has a gradient)."""
@@ -58,7 +58,8 @@ class AdamW(torch.optim.Optimizer):
                 if st and "step" in st:
                     t = float(st["step"])
                     break
-            self._sched.append(torch.tensor([group["lr"], t, 0.0, 0.0], dtype=torch.float64, device=dev))
+            # {lr, t, lr/(1-b1^t), sqrt(1-b2^t), arrival counter of the advancing launch}
+            self._sched.append(torch.tensor([group["lr"], t, 0.0, 0.0, 0.0], dtype=torch.float64, device=dev))
             self._sched_lr.append(group["lr"])
 
     def _ensure_flat_state(self):
@@ -162,16 +163,19 @@ class AdamW(torch.optim.Optimizer):
             self._sched_lr[gi] = group["lr"]
         for p in params:
             self._init_state(p)
-        if sched_step:
-            ops.adamw_sched_step(sched, b1, b2)
+        # the first update launch of the step advances the schedule itself
+        # (ssip_adamw_dev advance=1); later launches read the advanced values
+        adv = sched_step
         for off, n, ps in runs:
             ops.adamw_dev(self.arena.flat[off:off + n], self.arena.grad[off:off + n],
                           self._flat_state[0][off:off + n], self._flat_state[1][off:off + n], sched,
-                          b1, b2, group["eps"], group["weight_decay"], grad_scale)
+                          b1, b2, group["eps"], group["weight_decay"], grad_scale, advance=adv)
+            adv = False
         for p in loose:
             st = self.state[p]
             ops.adamw_dev(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], sched, b1, b2,
-                          group["eps"], group["weight_decay"], grad_scale)
+                          group["eps"], group["weight_decay"], grad_scale, advance=adv)
+            adv = False
         increment_version(params)
 
     def device_step_count(self, gi: int = 0) -> int:

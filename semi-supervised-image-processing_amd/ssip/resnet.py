@@ -399,6 +399,49 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
     return _ConvRec(geom=g, conv=conv, bn=bn, x=x, y=y, stats=stats)
 
 
+def _conv_bn_ds(model: SSIPResNet, conv, bn, ds_conv, ds_bn, x: torch.Tensor, N, H, W, train: bool, save: bool,
+                update_running: bool) -> Tuple[_ConvRec, _ConvRec]:
+    """_conv_bn of a downsampling block's conv1 and of its 1x1 downsample in
+    one fused launch (ops.conv_fwd_ds): same input, same output grid."""
+    g = _geom(conv, N, H, W)
+    gd = _geom(ds_conv, N, H, W)
+    dt = model.compute_dtype
+    krsc = _prepped(model, conv, g, need_t=save)[0]
+    kds = _prepped(model, ds_conv, gd, need_t=save)[0]
+    recs = []
+    ys, parts, stats = [], [], []
+    for gg in (g, gd):
+        ys.append(torch.empty((N, gg.P, gg.Q, gg.K), device=x.device, dtype=dt))
+        stats.append(torch.empty((4, gg.K), device=x.device, dtype=torch.float32))
+        parts.append(torch.empty(ops.conv_fwd_partial_floats(gg), device=x.device, dtype=torch.float32)
+                     if train else None)
+    ops.conv_fwd_ds(g, x, krsc, ys[0], parts[0], gd, kds, ys[1], parts[1])
+    tiles = (ops.conv_fwd_partial_tiles(g, dt), ops.conv_fwd_ds_partial_tiles(g, gd, dt))
+    for gg, c, b, y, part, st, nt in zip((g, gd), (conv, ds_conv), (bn, ds_bn), ys, parts, stats, tiles):
+        if train:
+            ops.bn_finalize(gg.K, nt, part, b.weight.detach(), b.bias.detach(), b.running_mean, b.running_var,
+                            b.momentum if b.momentum is not None else 0.1, b.eps, update_running, st[0], st[1],
+                            st[2], st[3])
+        else:
+            ops.bn_eval_coeffs(gg.K, b.weight.detach(), b.bias.detach(), b.running_mean, b.running_var, b.eps,
+                               st[0], st[1], st[2], st[3])
+        recs.append(_ConvRec(geom=gg, conv=c, bn=b, x=x, y=y, stats=st))
+    return recs[0], recs[1]
+
+
+def _fwd_ds_fusable(blk, N: int, H: int, W: int) -> bool:
+    """BasicBlock conv1 (3x3, pad 1, stride s) + downsample (1x1, stride s): ops.conv_fwd_ds."""
+    if _NO_FWD_DS or blk.downsample is None or not isinstance(blk, BasicBlock):
+        return False
+    g = _geom(blk.conv1, N, H, W)
+    gd = _geom(blk.downsample[0], N, H, W)
+    return (g.R, g.S, g.pad, gd.R, gd.S, gd.pad, gd.stride) == (3, 3, 1, 1, 1, 0, g.stride) and \
+        (g.P, g.Q, g.K, g.C) == (gd.P, gd.Q, gd.K, gd.C)
+
+
+_NO_FWD_DS = os.environ.get("SSIP_NO_FWD_DSFUSE") == "1"
+
+
 def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, in_pad: int = 0) -> _Saved:
     N, H, W, C4 = images.shape
     dt = model.compute_dtype
@@ -449,8 +492,14 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
         z = x
         h, w = Hc, Wc
         stages = blk.stages()
+        ds = None
+        fuse_ds = _fwd_ds_fusable(blk, N, Hc, Wc)
         for i, (conv, bn) in enumerate(stages):
-            r = _conv_bn(model, conv, bn, z, N, h, w, train, save, upd)
+            if i == 0 and fuse_ds:
+                r, ds = _conv_bn_ds(model, conv, bn, blk.downsample[0], blk.downsample[1], z, N, h, w, train, save,
+                                    upd)
+            else:
+                r = _conv_bn(model, conv, bn, z, N, h, w, train, save, upd)
             h, w = r.geom.P, r.geom.Q
             if i < len(stages) - 1:
                 zz = torch.empty_like(r.y)
@@ -459,14 +508,14 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
                 z = zz
             recs.append(r)
         last = recs[-1]
-        ds = None
         out = torch.empty_like(last.y)
         # the backward masks with 1 bit per element instead of re-reading out
         bits = torch.empty(out.numel() // 8, device=dev, dtype=torch.uint8) if save else None
         if blk.downsample is not None:
             # out = relu(bn2(y2) + bn_ds(y_ds)): the downsample's BN is formed in
             # registers by the same pass (its output is never stored)
-            ds = _conv_bn(model, blk.downsample[0], blk.downsample[1], x, N, Hc, Wc, train, save, upd)
+            if ds is None:
+                ds = _conv_bn(model, blk.downsample[0], blk.downsample[1], x, N, Hc, Wc, train, save, upd)
             ops.bn_apply2(N * h * w, last.geom.K, last.y, last.stats[2], last.stats[3], ds.y, ds.stats[2],
                           ds.stats[3], True, out, bits)
         else:

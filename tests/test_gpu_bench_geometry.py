@@ -33,7 +33,7 @@ CONVS = [
     ("l2.ds", (64, 56, 128, 1, 2, 0), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad"}),
     ("l3.0.conv1", (128, 28, 256, 3, 2, 1), {"fwd": "glds<fwd", "dgrad": "glds<dgrad,128x128,4x2,2,phased",
                                              "wgrad": "glds<wgrad"}),
-    ("l3.3x3", (256, 14, 256, 3, 1, 1), {"fwd": "glds<fwd,256x256,4x2,2", "dgrad": "glds<dgrad,128x128",
+    ("l3.3x3", (256, 14, 256, 3, 1, 1), {"fwd": "glds<fwd,256x256,4x2,2", "dgrad": "glds<dgrad,256x256,4x2,2",
                                          "wgrad": "glds<wgrad,128x128"}),
     ("l3.ds", (128, 28, 256, 1, 2, 0), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad"}),
     ("l4.0.conv1", (256, 14, 512, 3, 2, 1), {"fwd": "glds<fwd", "dgrad": "glds<dgrad,128x128,4x2,2,phased",

@@ -206,6 +206,61 @@ def test_adamw_matches_torch(dev):
     assert _rel(p, ref.detach()) < 1e-6
 
 
+def test_adamw_device_schedule_fused_advance(dev):
+    """ssip_adamw_dev with advance=1 (ABI 8: the first update launch of a step
+    advances t and the bias corrections itself) equals the separate
+    ssip_adamw_sched_step + ssip_adamw_dev(advance=0) launches bit for bit,
+    through ssip.optim.AdamW's device schedule over 5 steps with several
+    launches per step (two arena runs, a loose parameter, a second group, and
+    a step split around one parameter as SemiStep does); both stay within
+    fp32 rounding of torch.optim.AdamW and count t like it."""
+    from ssip.arena import ParamArena
+    from ssip.optim import AdamW
+
+    torch.manual_seed(0)
+    shapes = [(300,), (17, 5), (1000,), (64,)]
+    base = [torch.randn(s) for s in shapes]
+    grads = [[torch.randn(s) for s in shapes] for _ in range(5)]
+    # reference: torch AdamW on the CPU
+    ref = [torch.nn.Parameter(b.clone()) for b in base]
+    topt = torch.optim.AdamW([{"params": [ref[0], ref[2]]}, {"params": [ref[1], ref[3]], "lr": 5e-4}], lr=1e-3,
+                             weight_decay=1e-2)
+    for gs in grads:
+        for p, g in zip(ref, gs):
+            p.grad = g.clone()
+        topt.step()
+    # fused path (AdamW.use_device_schedule)
+    ps = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    arena = ParamArena(ps[:3])
+    opt = AdamW([ps[0], ps[2]], lr=1e-3, weight_decay=1e-2, arena=arena)
+    opt.add_param_group({"params": [ps[1], ps[3]], "lr": 5e-4})  # ps[3] is not in the arena
+    opt.use_device_schedule()
+    for t, gs in enumerate(grads):
+        for p, g in zip(ps, gs):
+            p.grad = arena.grad_view(p) if arena.owns(p) else torch.empty_like(p)
+            p.grad.copy_(g.to(dev))
+        if t == 2:  # split step: everything but ps[0], then ps[0] alone
+            opt.step(skip={id(ps[0])}, join_pending=False)
+            opt.step(only={id(ps[0])}, sched_step=False)
+        else:
+            opt.step()
+    # the separate schedule launch, by hand
+    qs = [b.clone().to(dev) for b in base]
+    mv = [(torch.zeros_like(q), torch.zeros_like(q)) for q in qs]
+    scheds = [torch.tensor([lr, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64, device=dev) for lr in (1e-3, 5e-4)]
+    for gs in grads:
+        for gi, idx in ((0, (0, 2)), (1, (1, 3))):
+            ops.adamw_sched_step(scheds[gi], 0.9, 0.999)
+            for k in idx:
+                ops.adamw_dev(qs[k], gs[k].to(dev).reshape(-1).reshape(qs[k].shape), mv[k][0], mv[k][1], scheds[gi],
+                              0.9, 0.999, 1e-8, 1e-2)
+    torch.cuda.synchronize()
+    assert opt.device_step_count(0) == 5 and opt.device_step_count(1) == 5
+    for k in range(4):
+        assert torch.equal(ps[k].detach().cpu(), qs[k].cpu()), k
+        assert _rel(ps[k].detach(), ref[k].detach()) < 1e-6, k
+
+
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])
 def test_weight_prep_batch_layouts(dev, dtname):
     """Batched prep == the per-tensor layouts (exact): KRSC / CRSK, zero

@@ -297,7 +297,7 @@ def test_pipelines_match_reference_run(dev, tmp_path, monkeypatch, kind):
     from src.training.supervised import run_supervised
 
     gold = GOLD["pipeline"]
-    spy = _MetricSpy(monkeypatch)
+    mspy = _MetricSpy(monkeypatch)
     data = tiny_dataset.make(tmp_path / "mri")
     w = tmp_path / "w.pt"
     torch.save(tiny_dataset.pretrained_state_dict(gold["weights_seed"]), w)
@@ -372,8 +372,8 @@ def test_pipelines_match_reference_run(dev, tmp_path, monkeypatch, kind):
         for k in ("train_loss", "val_loss"):
             assert _rel(h[stage][k], hr[stage][k]) < 2e-3, (stage, k, h[stage][k], hr[stage][k])
         # train_acc / train_f1 / val_acc / val_f1: one flipped prediction at most
-        call = spy.check_history(h[stage], hr[stage], call, stage)
-    assert call == len(spy.calls)
+        call = mspy.check_history(h[stage], hr[stage], call, stage)
+    assert call == len(mspy.calls)
     op, opr = art["operating_point"], ref["operating_point"]
     assert list(op) == list(opr)
     for k in op:

@@ -30,6 +30,27 @@ for s, e in iv[1:]:
         ce = max(ce, e)
 u += ce - cs
 print(f"  any stream busy {u / 1e3:.1f} us, all idle {(t1 - t0 - u) / 1e3:.1f} us")
+# the all-idle intervals (no kernel of any stream running), largest first, with
+# the kernel that ended before and the one that started after
+idle = []
+cs, ce, last = iv[0][0], iv[0][1], None
+ends_at = {}
+for r in step:
+    ends_at.setdefault(int(r["End_Timestamp"]), r["Kernel_Name"])
+for s, e in iv[1:] + [(t1, t1)]:
+    if s > ce:
+        before = max((r for r in step if int(r["End_Timestamp"]) <= s), key=lambda r: int(r["End_Timestamp"]))
+        after = min((r for r in rows if int(r["Start_Timestamp"]) >= s), key=lambda r: int(r["Start_Timestamp"]),
+                    default=None)
+        idle.append(((s - ce) / 1e3, (ce - t0) / 1e3, before["Kernel_Name"][:40],
+                     after["Kernel_Name"][:40] if after else "-"))
+        cs, ce = s, e
+    else:
+        ce = max(ce, e)
+idle.sort(reverse=True)
+print(f"  all-idle intervals: {len(idle)}, largest:")
+for g in idle[:8]:
+    print("    %7.1f us at %8.1f  %s -> %s" % g)
 main = max(by.values(), key=len)
 gaps = sorted(((int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3, a["Kernel_Name"][:48],
                b["Kernel_Name"][:48]) for a, b in zip(main, main[1:]))[::-1]

@@ -72,6 +72,9 @@ def parse():
                     help="CPU-baseline warm-up steps (BASELINE.md section 3 asks >= 10: pass --cpu-warmup 10 "
                          "--cpu-steps 50 for the full protocol, ~6-7 min on 16 host cores)")
     ap.add_argument("--cpu-steps", type=int, default=4, help="CPU-baseline timed steps (median reported)")
+    ap.add_argument("--max-inflight", type=int, default=None,
+                    help="host waits for step k - N before enqueueing step k (0: never; default: SemiStep's own "
+                         "bound on launch-plan replays, $SSIP_MAX_INFLIGHT or 2)")
     return ap.parse_args()
 
 
@@ -220,6 +223,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.max_inflight is not None:
+        step.max_inflight = args.max_inflight
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step(x_l, y_l, x_u)

@@ -92,6 +92,19 @@ class SemiStep:
         self.plan = plan
         self._plan = None
         self._static_pbase = None
+        # launch-plan replays the host may have enqueued ahead of the device:
+        # with no bound the host fills HIP's queue, blocks, and resumes only
+        # after the device has drained most of it -- the device then idles
+        # ~0.3 ms per step (MI355X, ROCm 7.2: 6.95 vs 6.55 ms/step at 2,
+        # tools/ab_inflight.sh).  0 = unbounded.
+        self.max_inflight = int(os.environ.get("SSIP_MAX_INFLIGHT", "2"))
+        self._inflight = []
+        # pinned staging of the per-step view parameters: a ring reused across
+        # steps (a fresh pin_memory() per step can allocate page-locked memory,
+        # which stalls the device queue), each slot reusable once the H2D copy
+        # that read it has run (its event)
+        self._pin_ring = []   # [(pinned buffer, event or None)]
+        self._pin_next = 0
         if graph or plan:
             self.opt.use_device_schedule()
         # single process, no graph capture: the optimizer overlaps the stem
@@ -113,8 +126,36 @@ class SemiStep:
         s = self.size
         parts = (draw_params_batch(Bl, s, False, self.gen), draw_params_batch(Bu, s, False, self.gen),
                  draw_params_batch(Bu, s, True, self.gen))
-        buf = torch.cat(parts).pin_memory()
+        rows = sum(p.shape[0] for p in parts)
+        buf = self._pinned(rows, parts[0].shape[1:], parts[0].dtype)
+        torch.cat(parts, out=buf)
         return (buf[:Bl], buf[Bl:Bl + Bu], buf[Bl + Bu:])
+
+    def _pinned(self, rows, tail, dtype) -> torch.Tensor:
+        """The next slot of the pinned ring, waited for and sized to [rows, *tail]."""
+        R = 4
+        if len(self._pin_ring) < R:
+            self._pin_ring = [(None, None)] * R
+        i = self._pin_next
+        self._pin_next = (i + 1) % R
+        buf, ev = self._pin_ring[i]
+        if ev is not None:
+            ev.synchronize()
+        if buf is None or buf.shape != (rows,) + tuple(tail) or buf.dtype != dtype:
+            buf = torch.empty((rows,) + tuple(tail), dtype=dtype).pin_memory()
+        self._pin_ring[i] = (buf, None)
+        return buf
+
+    def _pinned_read(self, t) -> None:
+        """Mark the ring slot holding host tensor t as read by the stream's latest copy."""
+        if t is None:
+            return
+        for i, (buf, _) in enumerate(self._pin_ring):
+            if buf is not None and buf.data_ptr() == t.data_ptr():
+                ev = torch.cuda.Event()
+                ev.record()
+                self._pin_ring[i] = (buf, ev)
+                return
 
     def input_slots(self):
         """The device buffers a recorded plan reads its batch from
@@ -196,6 +237,7 @@ class SemiStep:
     def _eager_step(self, x_l, y_l, x_u, params) -> StepStats:
         dev = x_l.device
         pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
+        self._pinned_read(_common_base(params))
         out = self._fwd_bwd(x_l, y_l, x_u, pl, pw, ps)
         scale = self.bucketer.finish() if self.bucketer is not None else 1.0
         # 6. optimizer
@@ -270,12 +312,20 @@ class SemiStep:
         base = _common_base(params)
         if base is not None and self._static_pbase is not None and base.shape == self._static_pbase.shape:
             self._static_pbase.copy_(base, non_blocking=True)
+            self._pinned_read(base)
         else:
             for dst, src in zip(self._static[3:], params):
                 dst.copy_(src, non_blocking=True)
         if self.bucketer is not None:
             self.bucketer.reset()
+        if self.max_inflight > 0:
+            while len(self._inflight) >= self.max_inflight:
+                self._inflight.pop(0).synchronize()
         self._plan.replay()
+        if self.max_inflight > 0:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._inflight.append(ev)
         # the replay's AdamW changed the weights behind torch's back: bump the
         # versions so an eager forward afterwards refreshes its weight copies
         increment_version(list(self.model.parameters()))

@@ -41,7 +41,7 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICRO
 
 
 def _round_of(path: str) -> int:
-    m = re.search(r"r(\d+)_pmc_traffic", os.path.basename(path))
+    m = re.match(r"r(\d+)_", os.path.basename(path))
     return int(m.group(1)) if m else -1
 
 

@@ -44,7 +44,8 @@ for r in rows:
                                                                           int(r["End_Timestamp"]))})
     d[r["Counter_Name"]] = float(r["Counter_Value"])
 ds = list(disp.values())
-idx = [i for i, d in enumerate(ds) if "adamw" in d["name"] and "sched" not in d["name"]]
+idx = [i for i, d in enumerate(ds) if "weight_prep_batch" in d["name"] and
+       (i == 0 or "weight_prep_batch" not in ds[i - 1]["name"])]  # the step head (1-2 launches)
 step = ds[idx[-2] + 1: idx[-1] + 1]
 agg = collections.defaultdict(lambda: collections.Counter())
 fam = collections.defaultdict(lambda: collections.Counter())

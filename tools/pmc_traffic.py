@@ -28,7 +28,8 @@ def family(n):
 
 def per_step(path, counter):
     rows = [r for r in csv.DictReader(open(path)) if r.get("Counter_Name", counter) == counter]
-    idx = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"] and "sched" not in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "weight_prep_batch" in r["Kernel_Name"] and
+           (i == 0 or "weight_prep_batch" not in rows[i - 1]["Kernel_Name"])]  # the step head (1-2 launches)
     a, b = idx[-2], idx[-1]
     fam = collections.Counter()
     for r in rows[a + 1:b + 1]:

@@ -35,7 +35,8 @@ def family(n):
     return "other:" + n[:50]
 
 
-ends = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"] and "sched" not in r["Kernel_Name"]]
+ends = [i for i, r in enumerate(rows) if "weight_prep_batch" in r["Kernel_Name"] and
+        (i == 0 or "weight_prep_batch" not in rows[i - 1]["Kernel_Name"])]  # the step head (1-2 launches)
 step = rows[ends[k - 1] + 1:ends[k] + 1]
 t0 = int(rows[ends[k - 1]]["End_Timestamp"])
 t1 = max(int(r["End_Timestamp"]) for r in step)

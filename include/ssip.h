@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 8
+#define SSIP_ABI_VERSION 9
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -132,7 +132,15 @@ int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* bu
 /* ------------------------------------------------------------------------
  * BatchNorm2d (train / eval) fused with ReLU and the residual add.
  * ---------------------------------------------------------------------- */
-int ssip_bn_finalize(int C, int tiles, const float* partial, const float* gamma, const float* beta,
+/* Batch statistics from `tiles` {count, sum, M2} records per channel
+ * ([C][tiles][3], as ssip_conv_fwd writes them) -> mean / invstd / scale /
+ * shift (+ the running statistics).  More than 2048 records per channel are
+ * split over several workgroups (ABI 9) whose fp64 partial results use
+ * ssip_bn_finalize_scratch_floats(C, tiles) floats behind the records (the
+ * records themselves are not modified); ssip_conv_fwd_partial_floats
+ * includes that tail. */
+int64_t ssip_bn_finalize_scratch_floats(int C, int tiles);
+int ssip_bn_finalize(int C, int tiles, float* partial, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int update_running,
                      float* mean_out, float* invstd_out, float* scale_out, float* shift_out, void* stream);
 int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
@@ -164,8 +172,9 @@ int ssip_bn_relu_bwd(int dtype, int64_t M, int C, const void* dz, const void* y,
                      float* dbeta, int accumulate, void* dy, float* partial, float* coef, void* stream);
 /* Finish a BN backward whose reduction came from ssip_conv_dgrad_bn's partials
  * ([tiles][C][2] sums of dout and dout*xhat; dout already ReLU-masked):
- * dgamma/dbeta (+)= ..., dy = dBN(dout). */
-int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const float* partial, const void* dout,
+ * dgamma/dbeta (+)= ..., dy = dBN(dout).  The split finalize's scratch sits
+ * behind the records (ssip_conv_dgrad_bn_partial_floats includes it). */
+int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, float* partial, const void* dout,
                               const void* y, const float* mean, const float* invstd, const float* gamma,
                               float* dgamma, float* dbeta, int accumulate, void* dy, float* coef, void* stream);
 int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out, void* stream);

@@ -21,52 +21,110 @@
 
 namespace {
 
-// One 1024-thread workgroup per channel, one pass over the per-tile
-// {count, sum, M2-about-tile-mean} records in fp64, shifted by the first
-// record's mean K (the shifted-data form of the pairwise merge):
+struct BnFwdFin {
+  const float *gamma, *beta;
+  float *running_mean, *running_var;
+  float momentum, eps;
+  int update_running;
+  float *mean_out, *invstd_out, *scale_out, *shift_out;
+};
+
+__device__ __forceinline__ void bn_fin_write(int c, const BnFwdFin& f, double N, double mu, double m2) {
+  const double var = N > 0.0 ? m2 / N : 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
+  const float scale = g * invstd;
+  f.mean_out[c] = (float)mu;
+  f.invstd_out[c] = invstd;
+  f.scale_out[c] = scale;
+  f.shift_out[c] = b - (float)mu * scale;
+  if (f.update_running) {
+    const double unbiased = N > 1 ? m2 / (N - 1) : var;
+    f.running_mean[c] = (float)((1.0 - f.momentum) * f.running_mean[c] + f.momentum * mu);
+    f.running_var[c] = (float)((1.0 - f.momentum) * f.running_var[c] + f.momentum * unbiased);
+  }
+}
+
+// Workgroup (s, c): split s of channel c's per-tile {count, sum,
+// M2-about-tile-mean} records in fp64, shifted by the split's first record's
+// mean K (the shifted-data form of the pairwise merge):
 //   n = sum n_t,  s = sum n_t (mean_t - K),  q = sum M2_t + n_t (mean_t - K)^2
 //   mean = K + s / n,  M2 = q - s^2 / n.
-// Threads take records t = tid, tid + 1024, ...; wave butterflies and a
-// 16-entry LDS combine in fixed order keep the result reproducible.
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(int C, int tiles, const float* __restrict__ partial,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, float* running_mean,
-                                                           float* running_var, float momentum, float eps,
-                                                           int update_running, float* mean_out, float* invstd_out,
-                                                           float* scale_out, float* shift_out) {
-  __shared__ double sh[3 * 16];
-  const int c = blockIdx.x;
+// Threads take FIN_PT records at a time, FIN_NT apart, in increasing order;
+// wave butterflies and a 4-entry LDS combine in fixed order keep the result
+// reproducible.  S == 1 writes the statistics; otherwise {n, mean, M2} of the
+// split go to scratch[c][s] for bn_finalize_merge_kernel.
+__global__ void __launch_bounds__(FIN_NT) bn_finalize_kernel(int C, int tiles, int S, const float* __restrict__ partial,
+                                                             double* scratch, BnFwdFin f) {
+  __shared__ double sh[3 * 4];
+  const int c = blockIdx.y, s = blockIdx.x;
   const float* rec = partial + (long)c * tiles * 3;
-  const double n0 = rec[0];
-  const double K = n0 > 0.0 ? (double)rec[1] / n0 : 0.0;
+  const int L = (tiles + S - 1) / S;
+  const int t0 = s * L, t1 = min(tiles, t0 + L);
+  double K = 0.0;
+  if (t0 < t1) {
+    const double n0 = rec[(long)t0 * 3];
+    K = n0 > 0.0 ? (double)rec[(long)t0 * 3 + 1] / n0 : 0.0;
+  }
   double v[3] = {0.0, 0.0, 0.0};
-  for (int t = threadIdx.x; t < tiles; t += 1024) {
-    const double nb = rec[(long)t * 3];
-    if (nb > 0.0) {
-      const double d = (double)rec[(long)t * 3 + 1] / nb - K;
-      v[0] += nb;
-      v[1] += nb * d;
-      v[2] += (double)rec[(long)t * 3 + 2] + nb * d * d;
+  for (int base = t0 + threadIdx.x; base < t1; base += FIN_NT * FIN_PT) {
+    float r[FIN_PT][3];
+#pragma unroll
+    for (int i = 0; i < FIN_PT; ++i) {
+      const int t = base + i * FIN_NT;
+      const bool ok = t < t1;
+      r[i][0] = ok ? rec[(long)t * 3] : 0.f;
+      r[i][1] = ok ? rec[(long)t * 3 + 1] : 0.f;
+      r[i][2] = ok ? rec[(long)t * 3 + 2] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FIN_PT; ++i) {
+      const double nb = r[i][0];
+      if (nb > 0.0) {
+        const double d = (double)r[i][1] / nb - K;
+        v[0] += nb;
+        v[1] += nb * d;
+        v[2] += (double)r[i][2] + nb * d * d;
+      }
     }
   }
-  block_sums_f64_1024<3>(v, sh);
+  block_sums_f64_256<3>(v, sh);
   if (threadIdx.x == 0) {
     const double N = v[0];
     const double mu = N > 0.0 ? K + v[1] / N : 0.0;
     const double m2 = N > 0.0 ? fmax(v[2] - v[1] * v[1] / N, 0.0) : 0.0;
-    const double var = m2 / N;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    const float scale = g * invstd;
-    mean_out[c] = (float)mu;
-    invstd_out[c] = invstd;
-    scale_out[c] = scale;
-    shift_out[c] = b - (float)mu * scale;
-    if (update_running) {
-      const double unbiased = N > 1 ? m2 / (N - 1) : var;
-      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
-      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+    if (S == 1) {
+      bn_fin_write(c, f, N, mu, m2);
+    } else {
+      double* o = scratch + ((long)c * S + s) * 3;
+      o[0] = N;
+      o[1] = mu;
+      o[2] = m2;
     }
+  }
+}
+
+// split finalize, second pass: one wave per channel merges the S split
+// {n, mean, M2} in a fixed butterfly, shifted by split 0's mean
+__global__ void __launch_bounds__(FIN_NT) bn_finalize_merge_kernel(int C, int S, const double* __restrict__ scratch,
+                                                                   BnFwdFin f) {
+  const int c = blockIdx.x * (FIN_NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  const double* in = scratch + (long)c * S * 3;
+  const double K = in[1];  // split 0's mean (0 when it is empty)
+  double v[3] = {0.0, 0.0, 0.0};
+  if (lane < S && in[lane * 3] > 0.0) {
+    const double n = in[lane * 3], d = in[lane * 3 + 1] - K;
+    v[0] = n;
+    v[1] = n * d;
+    v[2] = in[lane * 3 + 2] + n * d * d;
+  }
+  wave_sums_f64<3>(v);
+  if (lane == 0) {
+    const double N = v[0];
+    const double mu = N > 0.0 ? K + v[1] / N : 0.0;
+    const double m2 = N > 0.0 ? fmax(v[2] - v[1] * v[1] / N, 0.0) : 0.0;
+    bn_fin_write(c, f, N, mu, m2);
   }
 }
 
@@ -293,22 +351,6 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_dual_kernel(long M, int C, 
   }
 }
 
-struct BnDualFin {
-  const float *partial[2], *gamma[2], *mean[2], *invstd[2];
-  float *dgamma[2], *dbeta[2], *coef[2];
-};
-
-// both finalizes in one launch: workgroup c < C for BN a, C + c for BN b
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_dual_kernel(int C, int blocks, long M, BnDualFin f,
-                                                                    int accumulate) {
-  __shared__ double sh[2 * 16];
-  const int s = blockIdx.x >= C ? 1 : 0;
-  const int c = blockIdx.x - s * C;
-  bn_bwd_finalize_body(c, C, blocks, M, 1, s ? f.partial[1] : f.partial[0], s ? f.gamma[1] : f.gamma[0],
-                       s ? f.mean[1] : f.mean[0], s ? f.invstd[1] : f.invstd[0], s ? f.dgamma[1] : f.dgamma[0],
-                       s ? f.dbeta[1] : f.dbeta[0], accumulate, s ? f.coef[1] : f.coef[0], sh);
-}
-
 // dy_a = A_a*dout + B_a*ya + C_a,  dy_b = A_b*dout + B_b*yb + C_b
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_apply_dual_kernel(int total8, int C, const T* __restrict__ dz,
@@ -383,16 +425,28 @@ static int bn_elem_grid(long total8) {
 
 extern "C" {
 
-int ssip_bn_finalize(int C, int tiles, const float* partial, const float* gamma, const float* beta,
+int ssip_bn_finalize(int C, int tiles, float* partial, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int update_running,
                      float* mean_out, float* invstd_out, float* scale_out, float* shift_out, void* stream) {
   SSIP_REQUIRE(C > 0 && tiles > 0 && partial && mean_out && invstd_out && scale_out && shift_out, SSIP_ERR_ARG,
                "ssip_bn_finalize: bad arguments");
   SSIP_REQUIRE(!update_running || (running_mean && running_var), SSIP_ERR_ARG, "running stats required");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(1024), 0, (hipStream_t)stream, C, tiles, partial, gamma, beta,
-                     running_mean, running_var, momentum, eps, update_running, mean_out, invstd_out, scale_out,
-                     shift_out);
+  hipStream_t st = (hipStream_t)stream;
+  const BnFwdFin f{gamma, beta, running_mean, running_var, momentum, eps, update_running,
+                   mean_out, invstd_out, scale_out, shift_out};
+  const int S = fin_splits(tiles);
+  double* scratch = fin_scratch(partial, (int64_t)C * tiles * 3);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S, (const float*)partial, scratch,
+                     f);
+  if (S > 1)
+    hipLaunchKernelGGL(bn_finalize_merge_kernel, dim3((C + FIN_NT / 64 - 1) / (FIN_NT / 64)), dim3(FIN_NT), 0, st,
+                       C, S, (const double*)scratch, f);
   return ::ssip::check_launch("bn_finalize");
+}
+
+int64_t ssip_bn_finalize_scratch_floats(int C, int tiles) {
+  if (C <= 0 || tiles <= 0) return -1;
+  return fin_scratch_floats(C, tiles, 3);
 }
 
 int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
@@ -433,8 +487,10 @@ int ssip_bn_apply2(int dtype, int64_t M, int C, const void* y, const float* scal
 }
 
 int64_t ssip_bn_bwd_dual_partial_floats(int64_t M, int C) {
-  const int64_t n = ssip_bn_bwd_partial_floats(M, C);
-  return n < 0 ? n : 2 * n;
+  if (M <= 0 || C <= 0 || C % 8 || C > 2048) return -1;
+  const int rows = bwd_rows_per_block(M, C);
+  const long blocks = (M + rows - 1) / rows;
+  return 2 * (blocks * (int64_t)C * 2 + fin_scratch_floats(C, blocks, 2));
 }
 
 int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mask_bits,
@@ -453,20 +509,17 @@ int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zm
   const int total8 = (int)(M * C / 8);
   float* pa = partial;
   float* pb = partial + (long)blocks * C * 2;
-  BnDualFin f;
-  f.partial[0] = pa; f.partial[1] = pb;
-  f.gamma[0] = gamma_a; f.gamma[1] = gamma_b;
-  f.mean[0] = mean_a; f.mean[1] = mean_b;
-  f.invstd[0] = invstd_a; f.invstd[1] = invstd_b;
-  f.dgamma[0] = dgamma_a; f.dgamma[1] = dgamma_b;
-  f.dbeta[0] = dbeta_a; f.dbeta[1] = dbeta_b;
-  f.coef[0] = coef; f.coef[1] = coef + 3 * C;
+  double* scratch = fin_scratch(partial, 2 * (int64_t)blocks * C * 2);
+  const int S = fin_splits(blocks);
+  BnBwdFin f;
+  f.set[0] = bn_bwd_fin_set(pa, gamma_a, mean_a, invstd_a, dgamma_a, dbeta_a, coef, scratch);
+  f.set[1] = bn_bwd_fin_set(pb, gamma_b, mean_b, invstd_b, dgamma_b, dbeta_b, coef + 3 * C,
+                            scratch + (int64_t)C * S * 2);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_dual_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, mask_bits, (const T*)ya, (const T*)yb, mean_a, invstd_a, mean_b, invstd_b, pa,
                        pb);
-    hipLaunchKernelGGL(bn_bwd_finalize_dual_kernel, dim3(2 * C), dim3(1024), 0, st, C, blocks, (long)M, f,
-                       accumulate);
+    launch_bn_bwd_finalize(st, C, blocks, (long)M, 1, 2, f, accumulate);
     hipLaunchKernelGGL(bn_bwd_apply_dual_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
                        (const T*)dz, (const T*)zmask, mask_bits, (const T*)ya, (const T*)yb, coef, coef + 3 * C, (T*)dy_a,
                        (T*)dy_b);
@@ -477,7 +530,8 @@ int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zm
 int64_t ssip_bn_bwd_partial_floats(int64_t M, int C) {
   if (M <= 0 || C <= 0 || C % 8 || C > 2048) return -1;
   const int rows = bwd_rows_per_block(M, C);
-  return ((M + rows - 1) / rows) * (int64_t)C * 2;
+  const long blocks = (M + rows - 1) / rows;
+  return blocks * (int64_t)C * 2 + fin_scratch_floats(C, blocks, 2);
 }
 
 static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* zmask, const uint8_t* mbits,
@@ -495,15 +549,17 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, blocks, (long)M, 1, partial, gamma, mean,
-                       invstd, dgamma, dbeta, accumulate, coef);
+    BnBwdFin f;
+    f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
+                              fin_scratch(partial, (int64_t)blocks * C * 2));
+    launch_bn_bwd_finalize(st, C, blocks, (long)M, 1, 1, f, accumulate);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
                        (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
 }
 
-int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const float* partial, const void* dout,
+int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, float* partial, const void* dout,
                               const void* y, const float* mean, const float* invstd, const float* gamma,
                               float* dgamma, float* dbeta, int accumulate, void* dy, float* coef, void* stream) {
   SSIP_REQUIRE(M > 0 && C > 0 && C % 8 == 0 && tiles > 0 && partial && dout && y && mean && invstd && dy && coef,
@@ -512,8 +568,10 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, const floa
                "ssip_bn_bwd_from_partials: unsupported size");
   hipStream_t st = (hipStream_t)stream;
   const int total8 = (int)(M * C / 8);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, tiles, (long)M, 0, partial, gamma, mean,
-                     invstd, dgamma, dbeta, accumulate, coef);
+  BnBwdFin f;
+  f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
+                            fin_scratch(partial, (int64_t)tiles * C * 2));
+  launch_bn_bwd_finalize(st, C, tiles, (long)M, 0, 1, f, accumulate);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
                        (const T*)nullptr, (const uint8_t*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr,

@@ -5,73 +5,150 @@
 //   dy = coef[c] * dout + coef[C+c] * y + coef[2C+c].
 #pragma once
 #include "ssip_common.h"
+#include "fin_split.h"
 
 namespace {
 
-// sums of up to three values over a 1024-thread workgroup in fp64 with one
-// LDS round (wave butterflies, then the 16 wave totals in fixed order)
+// Finalize workgroups: 256 threads (one wave per SIMD), so a finalize
+// launched beside a running convolution finds room as soon as any conv
+// workgroup retires (a 1024-thread workgroup waited for a whole CU: 30-150 us
+// on the forward critical path in the round-3 step trace).  A channel whose
+// records would take more than FIN_PT per thread is split over S workgroups
+// (fin_splits); their fp64 partial results go to a scratch area behind the
+// records (fin_scratch) and a one-wave-per-channel merge finishes them.
+// sums of up to three values over a 256-thread workgroup in fp64 with one
+// LDS round (wave butterflies, then the 4 wave totals in fixed order)
 template <int V>
-__device__ __forceinline__ void block_sums_f64_1024(double (&v)[V], double* sh) {
+__device__ __forceinline__ void block_sums_f64_256(double (&v)[V], double* sh) {
 #pragma unroll
   for (int k = 0; k < V; ++k)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int k = 0; k < V; ++k) sh[k * 16 + (threadIdx.x >> 6)] = v[k];
+    for (int k = 0; k < V; ++k) sh[k * 4 + (threadIdx.x >> 6)] = v[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < V; ++k) {
-    double t = 0.0;
+  for (int k = 0; k < V; ++k) v[k] = ((sh[k * 4] + sh[k * 4 + 1]) + sh[k * 4 + 2]) + sh[k * 4 + 3];
+}
+
+// sums of V values over one wave (every lane ends with the same bits)
+template <int V>
+__device__ __forceinline__ void wave_sums_f64(double (&v)[V]) {
 #pragma unroll
-    for (int w = 0; w < 16; ++w) t += sh[k * 16 + w];
-    v[k] = t;
-  }
+  for (int k = 0; k < V; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
 }
 
-// One 1024-thread workgroup per channel: sums of dout and dout*xhat over the
-// partials (threads take blocks t = tid, tid + 1024, ...); cmajor: [C][blocks][2]
-// (each channel's records contiguous), else [blocks][C][2].
-__device__ __forceinline__ void bn_bwd_finalize_body(int c, int C, int blocks, long M, int cmajor,
-                                                     const float* __restrict__ partial,
-                                                     const float* __restrict__ gamma, const float* __restrict__ mean,
-                                                     const float* __restrict__ invstd, float* dgamma, float* dbeta,
-                                                     int accumulate, float* coef, double* sh) {
-  double ab[2] = {0.0, 0.0};
+// One BatchNorm's backward finalize operands
+struct BnBwdFinSet {
+  const float *partial, *gamma, *mean, *invstd;
+  float *dgamma, *dbeta, *coef;
+  double* scratch;  // [C][S][2] when S > 1
+};
+struct BnBwdFin {
+  BnBwdFinSet set[2];
+};
+
+__device__ __forceinline__ void bn_bwd_fin_write(int c, int C, long M, const BnBwdFinSet& f, int accumulate,
+                                                 double sum_d, double sum_dx) {
+  if (f.dgamma) f.dgamma[c] = (float)(accumulate ? f.dgamma[c] + sum_dx : sum_dx);
+  if (f.dbeta) f.dbeta[c] = (float)(accumulate ? f.dbeta[c] + sum_d : sum_d);
+  const double g = f.gamma ? f.gamma[c] : 1.0;
+  const double is = f.invstd[c];
+  const double A = g * is;
+  const double k0 = -A * sum_d / (double)M;
+  const double k1 = -A * sum_dx / (double)M * is;
+  f.coef[c] = (float)A;                             // * dout
+  f.coef[C + c] = (float)k1;                        // * y
+  f.coef[2 * C + c] = (float)(k0 - k1 * f.mean[c]);  // constant
+}
+
+// Workgroup (s, set * C + c): sums of dout and dout*xhat over split s of the
+// channel's partials (threads take FIN_PT records at a time, FIN_NT apart, in
+// increasing order); cmajor: [C][blocks][2] (each channel's records
+// contiguous), else [blocks][C][2].  S == 1 writes the outputs directly.
+__global__ void __launch_bounds__(FIN_NT) bn_bwd_finalize_kernel(int C, int blocks, int S, long M, int cmajor,
+                                                                 BnBwdFin fin, int accumulate) {
+  __shared__ double sh[2 * 4];
+  const int set = blockIdx.y >= C ? 1 : 0;
+  const int c = blockIdx.y - set * C, s = blockIdx.x;
+  const BnBwdFinSet& f = fin.set[set];
+  const int L = (blocks + S - 1) / S;
+  const int t0 = s * L, t1 = min(blocks, t0 + L);
   const long cs = cmajor ? 2 : (long)C * 2;
-  const float* pc = partial + (cmajor ? (long)c * blocks * 2 : (long)c * 2);
-  for (int t = threadIdx.x; t < blocks; t += 1024) {
-    ab[0] += pc[t * cs + 0];
-    ab[1] += pc[t * cs + 1];
+  const float* pc = f.partial + (cmajor ? (long)c * blocks * 2 : (long)c * 2);
+  double ab[2] = {0.0, 0.0};
+  for (int base = t0 + threadIdx.x; base < t1; base += FIN_NT * FIN_PT) {
+    float r[FIN_PT][2];
+#pragma unroll
+    for (int i = 0; i < FIN_PT; ++i) {
+      const int t = base + i * FIN_NT;
+      r[i][0] = t < t1 ? pc[t * cs + 0] : 0.f;
+      r[i][1] = t < t1 ? pc[t * cs + 1] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FIN_PT; ++i) {
+      ab[0] += r[i][0];
+      ab[1] += r[i][1];
+    }
   }
-  block_sums_f64_1024<2>(ab, sh);
-  const double sum_d = ab[0], sum_dx = ab[1];
+  block_sums_f64_256<2>(ab, sh);
   if (threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + sum_dx : sum_dx);
-    if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + sum_d : sum_d);
-    const double g = gamma ? gamma[c] : 1.0;
-    const double is = invstd[c];
-    const double A = g * is;
-    const double k0 = -A * sum_d / (double)M;
-    const double k1 = -A * sum_dx / (double)M * is;
-    coef[c] = (float)A;                           // * dout
-    coef[C + c] = (float)k1;                      // * y
-    coef[2 * C + c] = (float)(k0 - k1 * mean[c]);  // constant
+    if (S == 1) {
+      bn_bwd_fin_write(c, C, M, f, accumulate, ab[0], ab[1]);
+    } else {
+      f.scratch[((long)c * S + s) * 2 + 0] = ab[0];
+      f.scratch[((long)c * S + s) * 2 + 1] = ab[1];
+    }
   }
 }
 
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(int C, int blocks, long M, int cmajor,
-                                                               const float* __restrict__ partial,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ mean,
-                                                               const float* __restrict__ invstd, float* dgamma,
-                                                               float* dbeta, int accumulate, float* coef) {
-  __shared__ double sh[2 * 16];
-  bn_bwd_finalize_body(blockIdx.x, C, blocks, M, cmajor, partial, gamma, mean, invstd, dgamma, dbeta, accumulate,
-                       coef, sh);
+// split finalize, second pass: one wave per (set, channel) adds the S split
+// sums in a fixed butterfly
+__global__ void __launch_bounds__(FIN_NT) bn_bwd_finalize_merge_kernel(int C, int sets, int S, long M, BnBwdFin fin,
+                                                                       int accumulate) {
+  const int w = blockIdx.x * (FIN_NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= sets * C) return;
+  const int set = w >= C ? 1 : 0;
+  const int c = w - set * C;
+  const BnBwdFinSet& f = fin.set[set];
+  double ab[2] = {0.0, 0.0};
+  if (lane < S) {
+    ab[0] = f.scratch[((long)c * S + lane) * 2 + 0];
+    ab[1] = f.scratch[((long)c * S + lane) * 2 + 1];
+  }
+  wave_sums_f64<2>(ab);
+  if (lane == 0) bn_bwd_fin_write(c, C, M, f, accumulate, ab[0], ab[1]);
 }
 
-static inline int bn_bwd_finalize_grid(int C) { return C; }
+// host: launch the (split) backward finalize of `sets` BatchNorms whose
+// records are `blocks` per channel
+static inline void launch_bn_bwd_finalize(hipStream_t st, int C, int blocks, long M, int cmajor, int sets,
+                                          const BnBwdFin& fin, int accumulate) {
+  const int S = fin_splits(blocks);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(S, sets * C), dim3(FIN_NT), 0, st, C, blocks, S, M, cmajor, fin,
+                     accumulate);
+  if (S > 1)
+    hipLaunchKernelGGL(bn_bwd_finalize_merge_kernel, dim3((sets * C + FIN_NT / 64 - 1) / (FIN_NT / 64)),
+                       dim3(FIN_NT), 0, st, C, sets, S, M, fin, accumulate);
+}
+
+static inline BnBwdFinSet bn_bwd_fin_set(const float* partial, const float* gamma, const float* mean,
+                                         const float* invstd, float* dgamma, float* dbeta, float* coef,
+                                         double* scratch) {
+  BnBwdFinSet f;
+  f.partial = partial;
+  f.gamma = gamma;
+  f.mean = mean;
+  f.invstd = invstd;
+  f.dgamma = dgamma;
+  f.dbeta = dbeta;
+  f.coef = coef;
+  f.scratch = scratch;
+  return f;
+}
 
 // Totals of V per-thread [8]-vectors over the threads that share a channel
 // chunk (tid % cpr, 256-thread block): a butterfly over the lane bits above

@@ -28,6 +28,7 @@
 // (bitwise reproducible, no atomics).
 #include <algorithm>
 #include "ssip_common.h"
+#include "fin_split.h"
 
 namespace {
 
@@ -3277,7 +3278,9 @@ int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d) {
   HaloPlan hp;  // one record per (channel, workgroup) on the halo path
   if (halo_plan(MODE_FWD, d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
   if (stem_plan(d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
-  return n;
+  // + the scratch of ssip_bn_finalize's split pass (the most records any
+  // plan writes bounds the splits; the scratch starts behind the records)
+  return n + fin_scratch_floats(d->K, n / (3 * d->K), 3);
 }
 
 int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void* w_krsc, void* y, float* bn_partial,
@@ -3427,7 +3430,8 @@ int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d) {
   if (plan_conv(MODE_DGRAD, d, 4, pl) != SSIP_OK) {
     if (plan_conv(MODE_DGRAD, d, 2, pl) != SSIP_OK) return -1;
   }
-  return (int64_t)ceil_div(pl.args.M, 128) * d->C * 2;
+  const long tiles = ceil_div(pl.args.M, 128);
+  return tiles * d->C * 2 + fin_scratch_floats(d->C, tiles, 2);  // + ssip_bn_bwd_from_partials' split scratch
 }
 
 int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype) {

@@ -1,0 +1,28 @@
+// Split of a BatchNorm finalize over several workgroups per channel (host and
+// device constants shared by bn_common.h and the partial-buffer sizing in
+// conv.hip / stem.hip / bn.hip).
+#pragma once
+#include <cstdint>
+
+namespace {
+
+constexpr int FIN_NT = 256;
+constexpr int FIN_PT = 8;
+constexpr int FIN_SMAX = 64;
+
+static inline int fin_splits(long tiles) {
+  long s = (tiles + FIN_NT * FIN_PT - 1) / (FIN_NT * FIN_PT);
+  return (int)(s < 1 ? 1 : (s > FIN_SMAX ? FIN_SMAX : s));
+}
+// floats the split finalize needs behind `records` floats of records (vals
+// fp64 values per (channel, split)); 0 when one workgroup per channel suffices
+static inline int64_t fin_scratch_floats(int C, long tiles, int vals) {
+  const int S = fin_splits(tiles);
+  return S > 1 ? 2 + (int64_t)C * S * vals * 2 : 0;
+}
+static inline double* fin_scratch(float* partial, int64_t records) {
+  uintptr_t p = (uintptr_t)(partial + records);
+  return (double*)((p + 7) & ~(uintptr_t)7);
+}
+
+}  // namespace

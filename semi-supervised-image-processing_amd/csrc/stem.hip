@@ -316,11 +316,13 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
 int64_t ssip_stem_pool_bn_bwd_partial_floats(int N, int H, int W, int C) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || 256 % (C / 8)) return -1;
   const int rows = rows_per_block(N, H);
-  const int64_t full = (int64_t)((N * H + rows - 1) / rows) * C * 2;
+  const long full = (N * H + rows - 1) / rows;
   // the pooled-grid reduction (ymax given): any pooled size <= the full-resolution one
   const long Mp = (long)N * H * W;
   const int prow = bwd_rows_per_block(Mp, C);
-  return std::max<int64_t>(full, (int64_t)((Mp + prow - 1) / prow) * C * 2);
+  const long blocks = std::max<long>(full, (Mp + prow - 1) / prow);
+  // + the split finalize's scratch (bn_common.h)
+  return blocks * C * 2 + fin_scratch_floats(C, blocks, 2);
 }
 
 int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* dpool,
@@ -352,8 +354,10 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
     else
       hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                          pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(bn_bwd_finalize_grid(C)), dim3(1024), 0, st, C, red_blocks, M, 1, partial, gamma, mean,
-                       invstd, dgamma, dbeta, accumulate, coef);
+    BnBwdFin f;
+    f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
+                              fin_scratch(partial, (int64_t)red_blocks * C * 2));
+    launch_bn_bwd_finalize(st, C, red_blocks, M, 1, 1, f, accumulate);
     if (dy)  // dy == nullptr: only dgamma/dbeta/coef (ssip_stem_bwd_wgrad forms dy on the fly)
       hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
                          (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);

@@ -29,7 +29,7 @@ def abi_version_expected() -> int:
     return int(m.group(1)) if m else ABI_VERSION
 
 
-ABI_VERSION = 8  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
+ABI_VERSION = 9  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1
@@ -96,6 +96,7 @@ _SIGS = {
     "ssip_stem_bwd_wgrad_supported": (_c_int, [_PD, _c_int]),
     "ssip_conv_kernel_name": (_c_int, [_c_int, _PD, _c_int, ctypes.c_char_p, _c_int]),
     "ssip_stem_bwd_wgrad": (_c_int, [_PD, _c_int] + [_vp] * 8 + [_c_int] * 3 + [_vp, _c_i64, _vp]),
+    "ssip_bn_finalize_scratch_floats": (_c_i64, [_c_int, _c_int]),
     "ssip_bn_finalize": (_c_int, [_c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_eval_coeffs": (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp, _vp]),
     "ssip_bn_apply": (_c_int, [_c_int, _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp]),

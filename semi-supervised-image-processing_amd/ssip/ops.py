@@ -368,6 +368,14 @@ def weight_prep(w: torch.Tensor, dtype: torch.dtype, Cp: int, Sp: int, krsc: Opt
 # ---------------------------------------------------------------------------
 # batch norm
 # ---------------------------------------------------------------------------
+def bn_finalize_scratch_floats(C: int, tiles: int) -> int:
+    """floats ssip_bn_finalize's split pass needs behind C*tiles*3 records"""
+    n = int(_lib.lib().ssip_bn_finalize_scratch_floats(C, tiles))
+    if n < 0:
+        raise ValueError(f"bn_finalize_scratch_floats: bad arguments C={C} tiles={tiles}")
+    return n
+
+
 def bn_finalize(C: int, tiles: int, partial, gamma, beta, running_mean, running_var, momentum: float, eps: float,
                 update_running: bool, mean, invstd, scale, shift) -> None:
     call("ssip_bn_finalize", C, tiles, _p(partial), _p(gamma), _p(beta), _p(running_mean), _p(running_var),

@@ -1,12 +1,14 @@
-#!/bin/bash
-# A/B of an environment setting in whole bench steps, alternated on one box.
-# usage: bash tools/ab_env.sh <tag> <rounds> "<A env assignments>" "<B env assignments>" [extra bench args]
+# A/B of environment settings on one box: bench ms/step, alternated runs.
+# usage: bash tools/ab_env.sh <tag> "<envA>" "<envB>" [rounds]
+#   e.g. bash tools/ab_env.sh fuse "SSIP_FUSE_BN_BWD=0" "SSIP_FUSE_BN_BWD=1" 3
 set -o pipefail
-tag=$1; rounds=$2; ea=$3; eb=$4; shift 4
-out=gpurun_out/$tag
-mkdir -p $out
-for i in $(seq 1 $rounds); do
-  env $ea timeout -k 10 200 python bench.py --no-cpu-baseline --steps 30 "$@" > $out/a$i.log 2>&1 || { tail -5 $out/a$i.log; exit 1; }
-  env $eb timeout -k 10 200 python bench.py --no-cpu-baseline --steps 30 "$@" > $out/b$i.log 2>&1 || { tail -5 $out/b$i.log; exit 1; }
+tag=$1; a=$2; b=$3; n=${4:-2}
+o=gpurun_out/ab_$tag
+mkdir -p $o
+for i in $(seq 1 $n); do
+  for side in A B; do
+    if [ $side = A ]; then e=$a; else e=$b; fi
+    env $e timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 > $o/$side$i.log 2>&1 || { echo "$side$i failed"; tail -5 $o/$side$i.log; exit 1; }
+    echo "$side [$e] run $i: $(tail -1 $o/$side$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
+  done
 done
-for f in $out/a*.log $out/b*.log; do echo $f $(grep -o '"ms_per_step": [0-9.]*' $f); done

@@ -2,7 +2,9 @@
 // device constants shared by bn_common.h and the partial-buffer sizing in
 // conv.hip / stem.hip / bn.hip).
 #pragma once
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 namespace {
 
@@ -10,8 +12,10 @@ constexpr int FIN_NT = 256;
 constexpr int FIN_PT = 8;
 constexpr int FIN_SMAX = 64;
 
+// (SSIP_FIN_PT: records per thread before a split, a tuning override)
 static inline int fin_splits(long tiles) {
-  long s = (tiles + FIN_NT * FIN_PT - 1) / (FIN_NT * FIN_PT);
+  static const long pt = getenv("SSIP_FIN_PT") ? std::max(1, atoi(getenv("SSIP_FIN_PT"))) : FIN_PT;
+  long s = (tiles + FIN_NT * pt - 1) / (FIN_NT * pt);
   return (int)(s < 1 ? 1 : (s > FIN_SMAX ? FIN_SMAX : s));
 }
 // floats the split finalize needs behind `records` floats of records (vals

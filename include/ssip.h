@@ -90,15 +90,23 @@ int ssip_conv_dgrad_ds(const ssip_conv_desc* d, int dtype, const void* dy, const
                        const void* wds_ck, void* dx, void* stream);
 /* DGRAD with the next-lower BatchNorm's backward reduction fused into the
  * epilogue (replaces ssip_conv_dgrad + the reduce pass of ssip_bn_bwd):
- *   dpre = (dgrad(dy) + dx_add) * (zmask > 0)          [N][H][W][C]
- *   partial[tile][c] = { sum dpre, sum dpre * (y - mean[c]) * invstd[c] }
- * zmask / y / mean / invstd belong to the BN+ReLU that produced this conv's
- * input; dx_add (nullable) may alias dpre. */
+ *   dpre = (dgrad(dy) + dx_add) * relu_mask                 [N][H][W][C]
+ *   partial[c][tile] = { sum dpre, sum dpre * (y - mean[c]) * invstd[c] }
+ * relu_mask (ABI 9: one source, first non-null wins): zmask > 0; bit c & 7 of
+ * mask_bits[pixel * C / 8 + c / 8] (ssip_bn_apply's mask bits); or
+ * fma(y, mscale, mshift) > 0 (a BN+ReLU with no residual: the forward's sign).
+ * y / mean / invstd belong to the BN+ReLU that produced this conv's input;
+ * dx_add (nullable) may alias dpre.  The 3x3 / stride-1 / 64-channel halo
+ * kernel takes mask_bits or mscale+mshift (not zmask); its records are one per
+ * (channel, workgroup, wave row).  Records per channel:
+ * ssip_conv_dgrad_bn_partial_tiles; ssip_conv_dgrad_bn_partial_floats sizes the
+ * buffer (records + the split finalize's scratch). */
 int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d);
 int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype);
 int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
-                       const void* zmask, const void* y, const float* mean, const float* invstd, void* dpre,
-                       float* partial, void* stream);
+                       const void* zmask, const uint8_t* mask_bits, const float* mscale, const float* mshift,
+                       const void* y, const float* mean, const float* invstd, void* dpre, float* partial,
+                       void* stream);
 /* Forward of a downsampling block's first conv (3x3, pad 1, stride s) and its
  * 1x1 / stride-s downsample (torchvision BasicBlock conv1 + downsample[0],
  * both `model(inputs)` at src/training/common.py:380) over the same input x:
@@ -171,7 +179,8 @@ int ssip_bn_relu_bwd(int dtype, int64_t M, int C, const void* dz, const void* y,
                      const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
                      float* dbeta, int accumulate, void* dy, float* partial, float* coef, void* stream);
 /* Finish a BN backward whose reduction came from ssip_conv_dgrad_bn's partials
- * ([tiles][C][2] sums of dout and dout*xhat; dout already ReLU-masked):
+ * ([C][tiles][2] sums of dout and dout*xhat, as ssip_conv_dgrad_bn writes
+ * them (ABI 9; was [tiles][C][2]); dout already ReLU-masked):
  * dgamma/dbeta (+)= ..., dy = dBN(dout).  The split finalize's scratch sits
  * behind the records (ssip_conv_dgrad_bn_partial_floats includes it). */
 int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, float* partial, const void* dout,

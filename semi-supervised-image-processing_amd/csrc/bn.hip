@@ -571,7 +571,7 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, float* par
   BnBwdFin f;
   f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
                             fin_scratch(partial, (int64_t)tiles * C * 2));
-  launch_bn_bwd_finalize(st, C, tiles, (long)M, 0, 1, f, accumulate);
+  launch_bn_bwd_finalize(st, C, tiles, (long)M, 1, 1, f, accumulate);
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
                        (const T*)nullptr, (const uint8_t*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr,

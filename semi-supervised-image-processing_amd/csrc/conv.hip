@@ -76,9 +76,15 @@ struct ConvArgs {
   const float* bias;   // FWD: per-output-channel bias (a folded eval-mode BatchNorm), nullable
   int relu;            // FWD: ReLU on the output (after bias and residual)
   // DGRAD post-op (BN backward of the layer that produced this conv's input):
-  // out = (dgrad + add) * (pmask > 0); per-(tile, channel) sums of out and
-  // out * (py - pmean) * pinvstd into partial [tiles_m][Ng][2].
+  // out = (dgrad + add) * relu_mask; per-(channel, tile) sums of out and
+  // out * (py - pmean) * pinvstd into partial [Ng][tiles_m][2].  The ReLU
+  // mask: pmask > 0 (z), else bit n & 7 of pbits[m * Ng / 8 + n / 8], else
+  // fma(py, pmscale, pmshift) > 0 (the forward's sign for a BN+ReLU with no
+  // residual).  Active when pmean != nullptr.
   const void* pmask;
+  const uint8_t* pbits;
+  const float* pmscale;
+  const float* pmshift;
   const void* py;
   const float* pmean;
   const float* pinvstd;
@@ -263,6 +269,7 @@ struct BnPostRegs {
   static constexpr int ROWS = BM / RPI;
   static_assert(NT % CPR == 0 && BM % RPI == 0, "thread count must cover whole rows");
   Vec8<T> z[ROWS], y[ROWS], add[ROWS];
+  uint32_t mb[ROWS];  // mask byte (pbits) of the thread's 8-channel chunk
 
   __device__ __forceinline__ void load(const ConvArgs& a, int m0, int n0) {
     const int tid = threadIdx.x;
@@ -277,7 +284,8 @@ struct BnPostRegs {
       const int m = m0 + rsub + k * RPI;
       if (m < a.M) {
         const long off = (long)m * a.Ng + n;
-        z[k].load(Zm + off);
+        if (Zm) z[k].load(Zm + off);
+        else if (a.pbits) mb[k] = a.pbits[off >> 3];
         y[k].load(Yp + off);
         if (Add) add[k].load(Add + off);
       }
@@ -297,14 +305,17 @@ __device__ __forceinline__ void dgrad_bn_post(const ConvArgs& a, char* smem, int
   const int n = n0 + ch * 8;
   T* Out = static_cast<T*>(a.out);
   const bool has_add = a.add != nullptr;
-  float sd[8], sx[8], mu[8], is[8];
+  float sd[8], sx[8], mu[8], is[8], msc[8], msh[8];
   const bool nok = n < a.Ng;
+  const int mode = a.pmask ? 0 : (a.pbits ? 1 : 2);  // mask source (ConvArgs)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sd[j] = 0.f;
     sx[j] = 0.f;
     mu[j] = nok ? a.pmean[n + j] : 0.f;
     is[j] = nok ? a.pinvstd[n + j] : 0.f;
+    msc[j] = (nok && mode == 2) ? a.pmscale[n + j] : 0.f;
+    msh[j] = (nok && mode == 2) ? a.pmshift[n + j] : 0.f;
   }
   if (nok) {
 #pragma unroll
@@ -324,7 +335,10 @@ __device__ __forceinline__ void dgrad_bn_post(const ConvArgs& a, char* smem, int
       for (int j = 0; j < 8; ++j) {
         float d = v.get(j);
         if (has_add) d += pr.add[k].get(j);
-        d = pr.z[k].get(j) > 0.f ? d : 0.f;
+        const bool keep = mode == 0 ? pr.z[k].get(j) > 0.f
+                                    : (mode == 1 ? ((pr.mb[k] >> j) & 1u) != 0u
+                                                 : __builtin_fmaf(pr.y[k].get(j), msc[j], msh[j]) > 0.f);
+        d = keep ? d : 0.f;
         v.set(j, d);
         const float dq = v.get(j);  // the stored (rounded) value feeds the sums
         sd[j] += dq;
@@ -363,7 +377,8 @@ __device__ __forceinline__ void dgrad_bn_post(const ConvArgs& a, char* smem, int
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) t += red[(w * CPR + c8) * 16 + v];
-      a.partial[((long)tm * a.Ng + nn + (v & 7)) * 2 + (v >> 3)] = t;
+      const int tiles_m = (a.M + BM - 1) / BM;  // [Ng][tiles_m][2]: each channel's records contiguous
+      a.partial[((long)(nn + (v & 7)) * tiles_m + tm) * 2 + (v >> 3)] = t;
     }
   }
 }
@@ -437,7 +452,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const ConvArgs& a, f32x4 (&ac
   }
   __syncthreads();
   if constexpr (MODE == MODE_DGRAD && ALLOW_POST) {
-    if (a.pmask != nullptr) {
+    if (a.pmean != nullptr) {
       if (pre_loaded) {
         dgrad_bn_post<T, BM, BN, NT>(a, smem, m0, n0, tm, pre);
       } else {
@@ -1756,6 +1771,15 @@ struct HaloArgs {
   uint32_t x_bytes, w_bytes, o_bytes;
   int N, H, W, Ncols, TR, tiles, units, flip;
   int dbg;  // ablation (tools/time_halo.py): 1 = no MFMA, 2 = no epilogue
+  // DGRAD BN-backward post-op (conv_halo_kernel<..., BNPOST>, ssip_conv_dgrad_bn):
+  // out = (dgrad + add) * relu_mask, and per-(channel, workgroup, wave row)
+  // sums {out, out * (y - mean) * invstd} into partial [Ncols][G][HALO_WMW][2].
+  // Mask: bit c & 7 of pbits[pixel * Ncols / 8 + c / 8], or (pbits null)
+  // fma(y, mscale, mshift) > 0.
+  const __bf16* py;
+  const uint8_t* pbits;
+  const float *pmean, *pinvstd, *pmscale, *pmshift;
+  uint32_t bits_bytes;
 };
 
 constexpr int HALO_XBUF = 44 * 1024;
@@ -1772,7 +1796,80 @@ __device__ __forceinline__ int xtile_off(int px, int slot) { return px * 128 + (
 // wait for the next tile's rows in flight and this tile's output stores
 __device__ __forceinline__ void halo_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }  // one input-row buffer: (TR + 2) * (W + 2) <= 352 pixels
 
-template <int WMW, int WNW, bool FOLD = false>
+// conv_halo_kernel's DGRAD epilogue with the BN-backward reduction of the
+// BN+ReLU below fused in (ssip_conv_dgrad_bn): per row-fragment i, the
+// residual-gradient add, y and the mask bytes of the lane's 4 x FN elements
+// are loaded together, then d = relu_mask ? bf16(bf16(acc) + add) : 0 is
+// stored and summed (d, d * (y - mean) * invstd) into the lane's columns.
+// Padded-grid rows (vmask clear) store nothing and add nothing.
+template <int FM, int FN, int BATCH, bool YONLY>
+__device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f32x4 (&acc)[FM][FN],
+                                                     __amdgpu_buffer_rsrc_t rsO, __amdgpu_buffer_rsrc_t rsA,
+                                                     __amdgpu_buffer_rsrc_t rsY, __amdgpu_buffer_rsrc_t rsM, int tile,
+                                                     int rows, int col0, const uint32_t (&rowoff)[FM][4],
+                                                     uint32_t vmask, int cbase, float (&bsd)[FN], float (&bsx)[FN]) {
+  typedef __bf16 T;
+  static_assert(FM % BATCH == 0, "row-group batches");
+  const uint32_t obase = (uint32_t)(((long)tile * rows * a.Ncols + col0) * 2);
+  float mu[FN], is[FN], msc[FN], msh[FN];
+  const bool bits = !YONLY && a.pbits != nullptr;  // YONLY: no add, mask from the BN affine
+  const bool has_add = !YONLY && a.add != nullptr;
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj) {
+    const int c = col0 + cbase + jj * 16;
+    mu[jj] = a.pmean[c];
+    is[jj] = a.pinvstd[c];
+    msc[jj] = bits ? 0.f : a.pmscale[c];
+    msh[jj] = bits ? 0.f : a.pmshift[c];
+  }
+  const int cbit = cbase & 7;  // column c's bit in its mask byte (jj * 16 keeps c & 7)
+  // the operands of BATCH row groups per round trip (all FM in one where the
+  // registers allow: each batch is a dependent HBM round trip per tile)
+#pragma unroll
+  for (int i0 = 0; i0 < FM; i0 += BATCH) {
+    short ra[BATCH][FN][4], ry[BATCH][FN][4];
+    uint32_t rm[BATCH][FN][4];
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = i0 + b;
+          const uint32_t off = obase + rowoff[i][e] + jj * 32;
+          const bool valid = (vmask >> (i * 4 + e)) & 1u;
+          ry[b][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsY, off, 0, 0);
+          ra[b][jj][e] = has_add ? __builtin_amdgcn_raw_buffer_load_b16(rsA, off, 0, 0) : (short)0;
+          rm[b][jj][e] =
+              bits ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsM, valid ? off >> 4 : SSIP_OOB, 0, 0) : 0u;
+        }
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = i0 + b;
+          const uint32_t off = obase + rowoff[i][e] + jj * 32;
+          const bool valid = (vmask >> (i * 4 + e)) & 1u;
+          const float yv = to_f32(__builtin_bit_cast(T, ry[b][jj][e]));
+          float t = to_f32(from_f32<T>(acc[i][jj][e]));
+          if (has_add) t += to_f32(__builtin_bit_cast(T, ra[b][jj][e]));
+          const bool keep = bits ? ((rm[b][jj][e] >> cbit) & 1u) != 0u : __builtin_fmaf(yv, msc[jj], msh[jj]) > 0.f;
+          const T o = from_f32<T>(keep ? t : 0.f);
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off, 0, 0);
+          const float dq = valid ? to_f32(o) : 0.f;
+          bsd[jj] += dq;
+          bsx[jj] += dq * ((yv - mu[jj]) * is[jj]);
+        }
+  }
+}
+
+// BNPOST: 0 = none; 1 = the BN-backward post-op with no residual add and the
+// mask from the BN affine (y is the only extra operand: one load batch per
+// tile); 2 = any other post-op operand set (one load batch per row group:
+// the registers hold no more without spilling)
+template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, NT = 64 * NW;
@@ -1836,14 +1933,20 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   // BN records [Ncols][G][WMW][3]: one per (channel, workgroup, wave row);
   // zero this workgroup's, then lanes < 16 of each wave keep the running
   // {n, mean, M2} of their FN columns over the wave's rows of every tile
+  constexpr int RV = BNPOST ? 2 : 3;  // floats per record
   if (a.partial) {
     for (int c = tid; c < a.Ncols * HALO_WMW; c += NT) {
-      float* rec = a.partial + ((long)(c / HALO_WMW) * G * HALO_WMW + (long)g * HALO_WMW + c % HALO_WMW) * 3;
-      rec[0] = 0.f;
-      rec[1] = 0.f;
-      rec[2] = 0.f;
+      float* rec = a.partial + ((long)(c / HALO_WMW) * G * HALO_WMW + (long)g * HALO_WMW + c % HALO_WMW) * RV;
+#pragma unroll
+      for (int v = 0; v < RV; ++v) rec[v] = 0.f;
     }
   }
+  // BNPOST: this lane's running sums {d, d * xhat} of its FN columns
+  float bsd[FN], bsx[FN];
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj) bsd[jj] = bsx[jj] = 0.f;
+  const __amdgpu_buffer_rsrc_t rsY = make_rsrc(a.py, BNPOST ? a.o_bytes : 0);
+  const __amdgpu_buffer_rsrc_t rsM = make_rsrc(a.pbits, BNPOST ? a.bits_bytes : 0);
   WaveStats<FM, FN> ws;
   ws.reset();
   // this lane's output rows (rbase + 16 i + e): byte offset within a tile's
@@ -1937,6 +2040,38 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     }
 
     // ---- epilogue
+    if constexpr (BNPOST) {
+      halo_bnpost_epilogue<FM, FN, BNPOST == 1 ? FM : 1, BNPOST == 1>(a, acc, rsO, rsA, rsY, rsM, tile, rows,
+                                                                          jn * BN, rowoff, vmask, cbase, bsd, bsx);
+      if (!prefetch) {
+        // panel / range end: the wave's column sums -> records [c][g][wm]
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int off = 16; off <= 32; off <<= 1) {
+            bsd[jj] += __shfl_xor(bsd[jj], off, 64);
+            bsx[jj] += __shfl_xor(bsx[jj], off, 64);
+          }
+        if (lane < 16) {
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj) {
+            const int c = jn * BN + cbase + jj * 16;
+            float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 2;
+            rec[0] = bsd[jj];
+            rec[1] = bsx[jj];
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj) bsd[jj] = bsx[jj] = 0.f;
+      }
+      if (more && !prefetch) {
+        halo_lds_barrier();
+        issue_w(jn_next);
+        issue_x(un - jn_next * a.tiles, Xn);
+        first = true;
+      }
+      continue;
+    }
     if (a.partial && wrows > 0) {
       // per-lane shifted sums over the fp32 accumulators of the valid rows;
       // merged across the wave (and written) when the panel or range ends
@@ -2937,7 +3072,7 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
     SSIP_GLDS_WG(SSIP_GLDS_GO)
   } else {
     if constexpr (MODE == MODE_DGRAD) {
-      if (pl.args.pmask != nullptr) {  // fused BN-backward epilogue: default tiles only
+      if (pl.args.pmean != nullptr) {  // fused BN-backward epilogue: default tiles only
 #define SSIP_GLDS_GOP(BM_, BN_, WM_, WN_, ST_)                                                                \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
     hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, true>), pl.grid,               \
@@ -3222,10 +3357,23 @@ static bool stem_wg_plan(const ssip_conv_desc* d, int dtype, HaloPlan& hp) {
   return true;
 }
 
+struct HaloBnPost {
+  const void* y;
+  const uint8_t* bits;
+  const float *mean, *invstd, *mscale, *mshift;
+};
+
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
                        void* out, const void* add, float* partial, hipStream_t st, const float* bias = nullptr,
-                       int relu = 0) {
+                       int relu = 0, const HaloBnPost* bp = nullptr) {
   HaloArgs h;
+  memset(&h, 0, sizeof(h));
+  if (bp) {
+    h.py = static_cast<const __bf16*>(bp->y);
+    h.pbits = bp->bits;
+    h.pmean = bp->mean; h.pinvstd = bp->invstd; h.pmscale = bp->mscale; h.pmshift = bp->mshift;
+    h.bits_bytes = (uint32_t)((long)d->N * d->H * d->W * hp.cols / 8);
+  }
   h.bias = bias;
   h.relu = relu;
   h.X = static_cast<const __bf16*>(X);
@@ -3253,7 +3401,11 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
       return SSIP_ERR_ARG;
     }
   }
-  if (bias != nullptr)  // folded eval BN epilogue
+  if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
+    hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
+  else if (bp != nullptr)
+    hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);
+  else if (bias != nullptr)  // folded eval BN epilogue
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
   else if (nw == 4)
     hipLaunchKernelGGL((conv_halo_kernel<4, 1>), dim3(hp.G), dim3(256), 0, st, h);
@@ -3430,24 +3582,19 @@ int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d) {
   if (plan_conv(MODE_DGRAD, d, 4, pl) != SSIP_OK) {
     if (plan_conv(MODE_DGRAD, d, 2, pl) != SSIP_OK) return -1;
   }
-  const long tiles = ceil_div(pl.args.M, 128);
+  long tiles = ceil_div(pl.args.M, 128);  // the LDS-DMA / register-staged paths: >= 128-row tiles
+  HaloPlan hp;
+  if (halo_plan(MODE_DGRAD, d, SSIP_BF16, hp)) tiles = std::max<long>(tiles, (long)hp.G * HALO_WMW);
   return tiles * d->C * 2 + fin_scratch_floats(d->C, tiles, 2);  // + ssip_bn_bwd_from_partials' split scratch
 }
 
-int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype) {
-  Plan pl;
-  if (plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
-  return ceil_div(pl.args.M, pl.bm);
-}
-
-int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
-                       const void* zmask, const void* y, const float* mean, const float* invstd, void* dpre,
-                       float* partial, void* stream) {
-  Plan pl;
+// the kernel ssip_conv_dgrad_bn runs: the halo kernel where it applies, else
+// the implicit-GEMM kernels at their 128-row tiles (no phase split)
+static int dgrad_bn_plan(const ssip_conv_desc* d, int dtype, Plan& pl, HaloPlan& hp, bool& halo) {
   int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
-  SSIP_REQUIRE(dy && w_crsk && zmask && y && mean && invstd && dpre && partial, SSIP_ERR_ARG,
-               "ssip_conv_dgrad_bn: null pointer");
+  halo = halo_plan(MODE_DGRAD, d, dtype, hp);
+  if (halo) return SSIP_OK;
   if (pl.stages > 0 && (d->stride != 1 || d->R * d->S > 32)) fallback_regstaged(pl);  // not phase-split here
   if (pl.stages > 0 && !getenv("SSIP_CONV_FORCE")) {  // the fused epilogue is built for the 128-row tiles only
     pl.bm = 128; pl.wmw = 4; pl.wnw = 2; pl.stages = 2;
@@ -3456,10 +3603,45 @@ int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const
     pl.grid = dim3(ceil_div(pl.args.M, pl.bm) * pl.args.tiles_n, 1, 1);
   }
   SSIP_REQUIRE(pl.bm >= 128, SSIP_ERR_ARG, "ssip_conv_dgrad_bn: partial sizing assumes >= 128-row tiles");
+  return SSIP_OK;
+}
+
+int ssip_conv_dgrad_bn_partial_tiles(const ssip_conv_desc* d, int dtype) {
+  Plan pl;
+  HaloPlan hp;
+  bool halo = false;
+  if (dgrad_bn_plan(d, dtype, pl, hp, halo) != SSIP_OK) return -1;
+  return halo ? hp.G * HALO_WMW : ceil_div(pl.args.M, pl.bm);
+}
+
+int ssip_conv_dgrad_bn(const ssip_conv_desc* d, int dtype, const void* dy, const void* w_crsk, const void* dx_add,
+                       const void* zmask, const uint8_t* mask_bits, const float* mscale, const float* mshift,
+                       const void* y, const float* mean, const float* invstd, void* dpre, float* partial,
+                       void* stream) {
+  Plan pl;
+  HaloPlan hp;
+  bool halo = false;
+  int rc = dgrad_bn_plan(d, dtype, pl, hp, halo);
+  if (rc) return rc;
+  SSIP_REQUIRE(dy && w_crsk && y && mean && invstd && dpre && partial, SSIP_ERR_ARG,
+               "ssip_conv_dgrad_bn: null pointer");
+  SSIP_REQUIRE(zmask || mask_bits || (mscale && mshift), SSIP_ERR_ARG,
+               "ssip_conv_dgrad_bn: one ReLU-mask source (zmask, mask_bits or mscale+mshift) is required");
+  SSIP_REQUIRE(d->C % 8 == 0, SSIP_ERR_ARG, "ssip_conv_dgrad_bn: C must be a multiple of 8");
+  if (halo) {
+    SSIP_REQUIRE(!zmask || mask_bits || (mscale && mshift), SSIP_ERR_ARG,
+                 "ssip_conv_dgrad_bn: the halo kernel takes mask bits or the BN affine, not z");
+    HaloBnPost bp;
+    bp.y = y; bp.bits = mask_bits; bp.mean = mean; bp.invstd = invstd;
+    bp.mscale = mask_bits ? nullptr : mscale; bp.mshift = mask_bits ? nullptr : mshift;
+    return launch_halo(MODE_DGRAD, d, hp, dy, w_crsk, dpre, dx_add, partial, (hipStream_t)stream, nullptr, 0, &bp);
+  }
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dpre; pl.args.add = dx_add;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
-  pl.args.pmask = zmask; pl.args.py = y; pl.args.pmean = mean; pl.args.pinvstd = invstd; pl.args.partial = partial;
+  pl.args.pmask = zmask; pl.args.pbits = zmask ? nullptr : mask_bits;
+  pl.args.pmscale = (zmask || mask_bits) ? nullptr : mscale; pl.args.pmshift = (zmask || mask_bits) ? nullptr : mshift;
+  pl.args.py = y; pl.args.pmean = mean; pl.args.pinvstd = invstd; pl.args.partial = partial;
   SSIP_DISPATCH_DTYPE(dtype, T, return launch_conv<MODE_DGRAD, T>(pl, (hipStream_t)stream));
 }
 

@@ -90,7 +90,7 @@ _SIGS = {
     "ssip_conv_fwd_bias": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp]),
     "ssip_conv_dgrad_bn_partial_floats": (_c_i64, [_PD]),
     "ssip_conv_dgrad_bn_partial_tiles": (_c_int, [_PD, _c_int]),
-    "ssip_conv_dgrad_bn": (_c_int, [_PD, _c_int] + [_vp] * 10),
+    "ssip_conv_dgrad_bn": (_c_int, [_PD, _c_int] + [_vp] * 13),
     "ssip_conv_wgrad_workspace_bytes": (_c_i64, [_PD]),
     "ssip_conv_wgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _vp]),
     "ssip_stem_bwd_wgrad_supported": (_c_int, [_PD, _c_int]),

@@ -279,20 +279,26 @@ def conv_dgrad_bn_partial_tiles(g: ConvGeom, dtype: torch.dtype) -> int:
 
 
 def conv_dgrad_bn(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx_add: Optional[torch.Tensor],
-                  zmask: torch.Tensor, y: torch.Tensor, mean: torch.Tensor, invstd: torch.Tensor,
-                  dpre: torch.Tensor, partial: torch.Tensor) -> None:
-    """dpre = (dgrad(dy) + dx_add) * (zmask > 0) plus the BN-backward partial
-    sums of the BN that produced zmask (see include/ssip.h)."""
+                  zmask: Optional[torch.Tensor], y: torch.Tensor, mean: torch.Tensor, invstd: torch.Tensor,
+                  dpre: torch.Tensor, partial: torch.Tensor, mask_bits: Optional[torch.Tensor] = None,
+                  mscale: Optional[torch.Tensor] = None, mshift: Optional[torch.Tensor] = None) -> None:
+    """dpre = (dgrad(dy) + dx_add) * relu_mask plus the BN-backward partial
+    sums ([C][tiles][2]) of the BN+ReLU below; the mask from zmask > 0, the
+    forward's mask bits, or fma(y, mscale, mshift) > 0 (see include/ssip.h)."""
     assert dy.numel() == g.N * g.P * g.Q * g.K, "conv_dgrad_bn: dy shape"
     assert w_crsk.numel() == g.K * g.R * g.S * g.C, "conv_dgrad_bn: w shape"
     n = g.N * g.H * g.W * g.C
-    assert dpre.numel() == n and zmask.numel() == n and y.numel() == n, "conv_dgrad_bn: activation shapes"
+    assert dpre.numel() == n and y.numel() == n, "conv_dgrad_bn: activation shapes"
+    assert zmask is None or zmask.numel() == n, "conv_dgrad_bn: zmask shape"
+    assert mask_bits is None or (mask_bits.dtype == torch.uint8 and mask_bits.numel() * 8 == n)
+    assert zmask is not None or mask_bits is not None or (mscale is not None and mshift is not None), \
+        "conv_dgrad_bn: a ReLU-mask source is required"
     assert mean.numel() >= g.C and invstd.numel() >= g.C and mean.dtype == invstd.dtype == torch.float32
     assert partial.dtype == torch.float32 and partial.numel() >= conv_dgrad_bn_partial_floats(g)
     if dx_add is not None:
         assert dx_add.numel() == n and dx_add.dtype == dpre.dtype
-    args = ("ssip_conv_dgrad_bn", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx_add), _p(zmask), _p(y),
-            _p(mean), _p(invstd), _p(dpre), _p(partial), stream_ptr())
+    args = ("ssip_conv_dgrad_bn", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx_add), _p(zmask),
+            _p(mask_bits), _p(mscale), _p(mshift), _p(y), _p(mean), _p(invstd), _p(dpre), _p(partial), stream_ptr())
     if _timer is not None:
         _timer.wrap("dgrad", g.flops(), call, *args)
         return

@@ -103,8 +103,25 @@ _DTYPES = {"fp32": torch.float32, "f32": torch.float32, "float32": torch.float32
 
 
 STEM_PAD = 3  # torchvision conv1 padding; the input producers pre-apply it
-# dgrad epilogue + BN-backward reduction fusion (ssip_conv_dgrad_bn); see _backward
-_FUSE_BN_BWD = os.environ.get("SSIP_FUSE_BN_BWD") == "1"
+# dgrad epilogue + BN-backward reduction fusion (ssip_conv_dgrad_bn); see _backward.
+# Default: where the dgrad runs on the halo kernel (layer 1: 3x3 / stride 1 / 64
+# channels) and the BN below has no residual add; SSIP_FUSE_BN_BWD=halo: every
+# halo dgrad, =1 everywhere, =0 nowhere.
+_FUSE_BN_BWD = os.environ.get("SSIP_FUSE_BN_BWD", "")
+_fuse_cache: dict = {}
+
+
+def _fuse_bn_bwd(g: ConvGeom, dt: torch.dtype, residual: bool = False) -> bool:
+    """residual: the BN below ends a block (mask bits + the identity gradient add)."""
+    if _FUSE_BN_BWD in ("0", "1"):
+        return _FUSE_BN_BWD == "1"
+    if residual and _FUSE_BN_BWD != "halo":
+        return False
+    key = (g, dt)
+    v = _fuse_cache.get(key)
+    if v is None:
+        v = _fuse_cache[key] = ops.conv_kernel_name("dgrad", g, dt).startswith("halo")
+    return v
 
 
 @dataclass
@@ -804,17 +821,24 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         crsk = _prepped_t(model, rec)[1]
         ops.conv_dgrad(rec.geom, dy, crsk, out, add)
 
-    def conv_dgrad_bn(rec: _ConvRec, dy, below: _ConvRec, out, add=None):
-        """dgrad of `rec` fused with the mask + BN reduction of `below` (the
-        BN+ReLU whose output z is rec's input).  Off by default: measured on
-        MI355X (tools/time_bnpost.py) the epilogue's extra z/y reads cost more
-        than the reduction pass they replace (l1: 272 vs 233 us)."""
-        if not _FUSE_BN_BWD:
+    def conv_dgrad_bn(rec: _ConvRec, dy, below: _ConvRec, out, add=None, residual: bool = False):
+        """dgrad of `rec` fused with the ReLU mask + BN-backward reduction of
+        `below` (the BN+ReLU whose output is rec's input): the mask from the
+        forward's mask bits where `below` ends a block (its ReLU follows the
+        residual add), else from y and below's BN affine.  Only where
+        _fuse_bn_bwd says so (the halo dgrads by default: the implicit-GEMM
+        epilogue costs more than the reduce pass it replaces)."""
+        if not _fuse_bn_bwd(rec.geom, dt, residual):
             conv_dgrad(rec, dy, out, add)
             return None
         crsk = _prepped_t(model, rec)[1]
         partial = torch.empty(ops.conv_dgrad_bn_partial_floats(rec.geom), device=dev, dtype=torch.float32)
-        ops.conv_dgrad_bn(rec.geom, dy, crsk, add, below.z, below.y, below.stats[0], below.stats[1], out, partial)
+        if residual:
+            zm, bits, msc, msh = (None, below.zbits, None, None) if below.zbits is not None else (below.z, None, None, None)
+        else:
+            zm, bits, msc, msh = None, None, below.stats[2], below.stats[3]
+        ops.conv_dgrad_bn(rec.geom, dy, crsk, add, zm, below.y, below.stats[0], below.stats[1], out, partial,
+                          mask_bits=bits, mscale=msc, mshift=msh)
         return out, partial, ops.conv_dgrad_bn_partial_tiles(rec.geom, dt)
 
     nblocks = len(sv.blocks)
@@ -859,10 +883,10 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             elif need_dx:
                 dxin = torch.empty_like(xin)
                 if ds is None and below is not None:
-                    pending = conv_dgrad_bn(r, g_cur, below, dxin, dpre)
+                    pending = conv_dgrad_bn(r, g_cur, below, dxin, dpre, residual=True)
                 elif ds is None:
                     conv_dgrad(r, g_cur, dxin, dpre)
-                elif _ds_dgrad_fusable(r.geom, ds.geom) and (below is None or not _FUSE_BN_BWD):
+                elif _ds_dgrad_fusable(r.geom, ds.geom) and (below is None or not _fuse_bn_bwd(ds.geom, dt, True)):
                     # conv1's and the downsample's input gradients in one launch
                     ops.conv_dgrad_ds(r.geom, g_cur, _prepped_t(model, r)[1], ds.geom, dy_ds,
                                       _prepped_t(model, ds)[1], dxin)
@@ -873,7 +897,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             conv_wgrad(ds, dy_ds)
             if dxin is not None and not ds_dgrad_done:
                 if below is not None:
-                    pending = conv_dgrad_bn(ds, dy_ds, below, dxin, dxin)
+                    pending = conv_dgrad_bn(ds, dy_ds, below, dxin, dxin, residual=True)
                 else:
                     conv_dgrad(ds, dy_ds, dxin, dxin)
         if hook is not None:

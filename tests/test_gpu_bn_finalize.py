@@ -77,12 +77,12 @@ def test_bn_finalize_split(dev, C, tiles, empty):
 
 @pytest.mark.parametrize("tiles", [512, 2049, 9408])
 def test_bn_bwd_from_partials_split(dev, tiles):
-    """[tiles][C][2] sums of dout and dout*xhat (the dgrad-fused BN reduction)
+    """[C][tiles][2] sums of dout and dout*xhat (the dgrad-fused BN reduction)
     -> dgamma / dbeta and dy = dBN(dout), split finalize included."""
     C, M = 64, 4096
     rng = np.random.default_rng(tiles)
-    p = rng.normal(0, 1, size=(tiles, C, 2)).astype(np.float32)
-    sums = p.astype(np.float64).sum(0)  # [C][2]
+    p = rng.normal(0, 1, size=(C, tiles, 2)).astype(np.float32)
+    sums = p.astype(np.float64).sum(1)  # [C][2]
     extra = 0 if tiles <= 2048 else 2 + C * 64 * 4
     part = torch.full((tiles * C * 2 + extra,), float("nan"), device=dev)
     part[:tiles * C * 2] = torch.from_numpy(p.reshape(-1)).to(dev)

@@ -139,17 +139,28 @@ def test_conv_wgrad(dev, shape, dtname):
     assert _relerr(dw.cpu(), 2 * ref) < tol
 
 
-@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3 and len(s) == 8])
+def _mask_bits(m_nhwc):
+    """bit j of byte i = element 8i + j of the NHWC-flat mask (ssip_bn_apply's layout)"""
+    f = m_nhwc.reshape(-1, 8).to(torch.int32)
+    return (f << torch.arange(8, dtype=torch.int32)).sum(1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] != 3 and len(s) == 8] + [(4, 64, 28, 28, 64, 3, 1, 1)])
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])
 @pytest.mark.parametrize("with_add", [False, True])
-def test_conv_dgrad_bn_fused(dev, shape, dtname, with_add):
+@pytest.mark.parametrize("mask", ["z", "bits", "affine"])
+def test_conv_dgrad_bn_fused(dev, shape, dtname, with_add, mask):
     """dgrad epilogue fused with the ReLU mask and the BN-backward partial
-    sums of the layer below: dpre = (dgrad + add) * (z > 0),
-    sum(dpre), sum(dpre * (y - mean) * invstd) per channel."""
+    sums of the layer below: dpre = (dgrad + add) * relu_mask,
+    sum(dpre), sum(dpre * (y - mean) * invstd) per channel ([C][tiles][2]).
+    The mask from z > 0, from the forward's mask bits, or from
+    fma(y, scale, shift) > 0; bf16 3x3 / stride-1 / 64-channel shapes run the
+    halo kernel (which takes bits or the affine)."""
     torch.manual_seed(3)
     N, C, H, W, K, R, st, pd = shape
     dt = torch.float32 if dtname == "f32" else torch.bfloat16
     g = _geom(*shape)
+    halo = ops.conv_kernel_name("dgrad", g, dt).startswith("halo")
     w = torch.randn(K, C, R, R) * 0.1
     dy = torch.randn(N, K, g.P, g.Q)
     add = torch.randn(N, C, H, W)
@@ -159,10 +170,18 @@ def test_conv_dgrad_bn_fused(dev, shape, dtname, with_add):
         w, dy, add, y, z = (t.bfloat16().float() for t in (w, dy, add, y, z))
     mean = torch.randn(C) * 0.1
     invstd = torch.rand(C) + 0.5
+    msc = torch.randn(C)
+    msh = torch.randn(C) * 0.5
+    if mask == "affine":
+        keep = (y.double() * msc.double()[None, :, None, None] + msh.double()[None, :, None, None]) > 0
+    else:
+        keep = z > 0
     ref = torch.nn.grad.conv2d_input((N, C, H, W), w.double(), dy.double(), stride=st, padding=pd)
     if with_add:
         ref = ref + add.double()
-    ref = ref * (z > 0).double()
+    if dt == torch.bfloat16:  # the stored dgrad (+ add) is bf16 before the mask and the sums
+        ref = ref.float().bfloat16().double()
+    ref = ref * keep.double()
     xhat = (y.double() - mean.double()[None, :, None, None]) * invstd.double()[None, :, None, None]
     sum_d = ref.sum((0, 2, 3))
     sum_dx = (ref * xhat).sum((0, 2, 3))
@@ -170,13 +189,21 @@ def test_conv_dgrad_bn_fused(dev, shape, dtname, with_add):
     ops.weight_prep(w.to(dev), dt, C, R, None, crsk)
     dpre = torch.empty((N, H, W, C), device=dev, dtype=dt)
     part = torch.full((ops.conv_dgrad_bn_partial_floats(g),), float("nan"), device=dev)
-    ops.conv_dgrad_bn(g, _to_nhwc(dy, K, dt, dev), crsk, _to_nhwc(add, C, dt, dev) if with_add else None,
-                      _to_nhwc(z, C, dt, dev), _to_nhwc(y, C, dt, dev), mean.to(dev), invstd.to(dev), dpre, part)
+    zh = _to_nhwc(z, C, dt, dev) if mask == "z" else None
+    bits = _mask_bits(keep.permute(0, 2, 3, 1).contiguous()).to(dev) if mask == "bits" else None
+    sc, sh = (msc.to(dev), msh.to(dev)) if mask == "affine" else (None, None)
+    args = (g, _to_nhwc(dy, K, dt, dev), crsk, _to_nhwc(add, C, dt, dev) if with_add else None, zh,
+            _to_nhwc(y, C, dt, dev), mean.to(dev), invstd.to(dev), dpre, part)
+    if halo and mask == "z":
+        with pytest.raises(RuntimeError, match="halo kernel takes mask bits"):
+            ops.conv_dgrad_bn(*args)
+        return
+    ops.conv_dgrad_bn(*args, mask_bits=bits, mscale=sc, mshift=sh)
     torch.cuda.synchronize()
     tol = 2e-5 if dt == torch.float32 else 1e-2
     assert _relerr(dpre.cpu(), ref.permute(0, 2, 3, 1)) < tol
     tiles = ops.conv_dgrad_bn_partial_tiles(g, dt)
-    p = part[: tiles * C * 2].view(tiles, C, 2).double().sum(0).cpu()
+    p = part[: tiles * C * 2].view(C, tiles, 2).double().sum(1).cpu()
     tol_s = 1e-4 if dt == torch.float32 else 2e-2
     assert _relerr(p[:, 0], sum_d) < tol_s
     assert _relerr(p[:, 1], sum_dx) < tol_s

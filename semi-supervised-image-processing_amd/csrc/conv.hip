@@ -3278,7 +3278,10 @@ static bool halo_plan(int mode, const ssip_conv_desc* d, int dtype, HaloPlan& hp
   hp.cols = cols;
   hp.tiles = (int)((long)d->N * d->H / TR);
   hp.units = hp.tiles * (cols / 64);
-  hp.G = std::min(hp.units, device_cus());
+  // persistent: one workgroup per CU (SSIP_HALO_GMUL: that many per CU, each
+  // over fewer tiles -- a tuning override)
+  static const int gmul = getenv("SSIP_HALO_GMUL") ? std::max(1, atoi(getenv("SSIP_HALO_GMUL"))) : 1;
+  hp.G = std::min(hp.units, gmul * device_cus());
   return true;
 }
 

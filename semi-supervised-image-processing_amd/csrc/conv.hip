@@ -917,8 +917,11 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 // 64-deep k-step covers filter rows 2ks and 2ks+1; k >= R*S*4 reads zeros.
 // POST: DGRAD with the BN-backward epilogue (ssip_conv_dgrad_bn); its
 // operand registers are only allocated in that instantiation.
+// LDIAG (timing experiments only, SSIP_LOOP_DIAG; results are wrong): 2-stage
+// k-loop with 1 = no MFMAs, 2 = no fragment reads, 4 = no LDS-DMA issue,
+// 8 = no barrier
 template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false,
-          bool FOLD = false>
+          bool FOLD = false, int LDIAG = 0>
 __global__ void __launch_bounds__(64 * WMW * WNW,
                                   (NSTAGE == 5 || NSTAGE == 8) ? 2
                                                                 : glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
@@ -1563,18 +1566,34 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   if (nsteps > 0) issue(0, 0);
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
+  Frag<T> fa[2][FM], fb[2][FN];
+  if constexpr ((LDIAG & 2) != 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) read_kfrag(fa[h][i], smem, i * 16 + (lane & 15), lane >> 4, h);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) read_kfrag(fb[h][j], smem, j * 16 + (lane & 15), lane >> 4, h);
+    }
+  }
   for (int ks = 0; ks < nsteps; ++ks) {
-    if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
-    if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
+    if constexpr ((LDIAG & 8) != 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
+    }
+    if constexpr ((LDIAG & 4) == 0) {
+      if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
+    }
     const char* As = smem + stage * STAGE;
     const char* Bs = As + A_BYTES;
     // both k-halves' fragments are requested before the first MFMA, so the
     // second half's LDS reads overlap the first half's matrix work
     // (wave tiles of more than 8 fragments read one k-half at a time)
     constexpr bool BOTH = FM + FN <= 8;
-    Frag<T> fa[2][FM], fb[2][FN];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      if ((LDIAG & 2) != 0) break;
       if (!BOTH && h == 1) break;
       if constexpr (!WG) {
 #pragma unroll
@@ -1590,7 +1609,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (!BOTH && h == 1) {
+      if ((LDIAG & 2) == 0 && !BOTH && h == 1) {
         if constexpr (!WG) {
 #pragma unroll
           for (int i = 0; i < FM; ++i) read_kfrag(fa[1][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, 1);
@@ -1603,10 +1622,17 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
           for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[1][j], Bs, wn * WTN + j * 16, lane, 1);
         }
       }
+      if constexpr ((LDIAG & 1) != 0) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(fa[h][i].v));
 #pragma unroll
-        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
+        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(fb[h][j].v));
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
+      }
     }
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
@@ -3067,6 +3093,26 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
     hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
                        st, pl.args);                                                                          \
     return ::ssip::check_launch("conv_glds");                                                                 \
+  }
+  {
+    // SSIP_LOOP_DIAG (timing experiments only): conv_glds_kernel's LDIAG ablations
+    static const int ldiag = getenv("SSIP_LOOP_DIAG") ? atoi(getenv("SSIP_LOOP_DIAG")) : 0;
+    if (ldiag && pl.args.pmean == nullptr && pl.args.bias == nullptr && !pl.conv1 && pl.stages == 2 &&
+        pl.wmw == 4 && pl.wnw == 2 && ((pl.bm == 128 && pl.bn == 128) || (pl.bm == 256 && pl.bn == 256))) {
+#define SSIP_GLDS_GOD(D_)                                                                                     \
+  if (ldiag == D_) {                                                                                          \
+    if (pl.bm == 128)                                                                                         \
+      hipLaunchKernelGGL((conv_glds_kernel<MODE, 128, 128, 4, 2, 2, false, false, false, D_>), pl.grid,      \
+                         dim3(512), 0, st, pl.args);                                                          \
+    else                                                                                                      \
+      hipLaunchKernelGGL((conv_glds_kernel<MODE, 256, 256, 4, 2, 2, false, false, false, D_>), pl.grid,      \
+                         dim3(512), 0, st, pl.args);                                                          \
+    return ::ssip::check_launch("conv_glds_diag");                                                            \
+  }
+      SSIP_GLDS_GOD(1) SSIP_GLDS_GOD(2) SSIP_GLDS_GOD(3) SSIP_GLDS_GOD(4) SSIP_GLDS_GOD(5) SSIP_GLDS_GOD(6)
+      SSIP_GLDS_GOD(8) SSIP_GLDS_GOD(12)
+#undef SSIP_GLDS_GOD
+    }
   }
   if constexpr (MODE == MODE_WGRAD) {
     SSIP_GLDS_WG(SSIP_GLDS_GO)

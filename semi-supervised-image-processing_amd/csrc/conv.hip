@@ -2175,6 +2175,264 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 }
 
 // ---------------------------------------------------------------------------
+// Row-balanced halo kernel (hb): 3x3 / stride 1 / pad 1 FWD and stride-1
+// DGRAD over >= 128 reduction channels (ResNet layers 2-4).
+//
+// Why (profiles/r3_loop_diag.txt): the implicit-GEMM ring kernel stages every
+// tap's A rows through LDS-DMA, so each input pixel crosses L2 -> LDS nine
+// times; at 128x128 tiles that is 15.6 B of DMA per kFLOP, and the per-CU
+// LDS-DMA intake (~68 GB/s) alone takes longer than the MFMAs (l3 fwd: DMA +
+// barrier only 53.7 us of a 73.9 us kernel).  Here the A operand of a 64-
+// channel chunk is one zero-haloed image of the tile's input rows, DMA'd
+// once for the chunk's nine taps (tap (r, s) of output pixel (n, p, q) is LDS
+// pixel base(n, p, q) + r (W+2) + s, as in conv_halo_kernel); only the
+// weights stream per k-step.  256 x BN tiles: ~5 B of DMA per kFLOP.
+//
+// Decomposition: one persistent workgroup per CU takes an equal contiguous
+// range of (column block, output pixel) units, cut into tiles of <= 256
+// pixels (ragged ends allowed: any pixel range has a halo window), so every
+// CU does the same MFMA work -- no wave-quantisation tail (layer 3 at batch
+// 256: 196 output rows per CU instead of 196 256x256 tiles on 256 CUs).
+//
+// k-loop: 9 taps x (Cr / 64) chunks, chunk-major; per k-step a counted wait +
+// barrier, then the next k-step's weights (2-stage ring) and, at a chunk's
+// first k-step, the next chunk's input window (2 buffers; the next tile's
+// first chunk during the tile's last) are issued before the MFMAs.
+// Epilogue as conv_halo_kernel: 16-bit stores from the accumulators (+ the
+// residual-gradient add for DGRAD), FWD BatchNorm records [Ncols][G][HALO_WMW][3]
+// per (channel, workgroup, wave row).  The k-order (chunk-major) differs from
+// conv_glds_kernel's (tap-major), so outputs agree to fp32 rounding.
+// ---------------------------------------------------------------------------
+struct HbArgs {
+  const __bf16* X;    // [N][H][W][Cr]  (FWD: x, DGRAD: dy)
+  const __bf16* Wt;   // [Ncols][9][Cr] (FWD: w_krsc, DGRAD: w_crsk)
+  __bf16* out;        // [N][H][W][Ncols]
+  const __bf16* add;  // DGRAD residual gradient (nullable, may alias out)
+  float* partial;     // FWD BN records (nullable)
+  uint32_t x_bytes, w_bytes, o_bytes;
+  int N, H, W, Cr, Ncols, M, flip;
+  long units;         // M * (Ncols / BN)
+  int dbg;            // timing ablations (tools): 1 = no MFMA
+};
+
+constexpr int HB_XBUF = 52 * 1024;  // one input window: <= 416 pixels x 128 B (host-checked)
+constexpr int HB_TM = 256;          // output pixels per tile
+
+// input window of the tile [m0, m0 + rows): padded rows n (H+2) + p + 1 of
+// input row p = -1 .. H of image n, from the first output row's p - 1 to the
+// last one's p + 1
+__device__ __forceinline__ void hb_window(const HbArgs& a, int m0, int rows, int& pr_lo, int& npx) {
+  const int HW = a.H * a.W, Hp = a.H + 2;
+  const int n0 = m0 / HW, p0 = (m0 - n0 * HW) / a.W;
+  const int m1 = m0 + rows - 1;
+  const int n1 = m1 / HW, p1 = (m1 - n1 * HW) / a.W;
+  pr_lo = n0 * Hp + p0;
+  npx = min((n1 * Hp + p1 + 3 - pr_lo) * (a.W + 2), HB_XBUF / 128);
+}
+
+template <int BN, int WNW>
+__global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
+  typedef __bf16 T;
+  constexpr int WMW = 4, NW = WMW * WNW, NT = 64 * NW;
+  constexpr int WTM = HB_TM / WMW, WTN = BN / WNW, FM = WTM / 16, FN = WTN / 16;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int IB = B_BYTES / 1024, LB = IB / NW;  // weight DMA instructions per k-step / per wave
+  static_assert(IB % NW == 0 && LB >= 1 && FM == 4 && FN >= 1 && WMW <= HALO_WMW, "hb tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * B_BYTES + 2 * HB_XBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int G = gridDim.x, g = blockIdx.x;
+  const long u0 = (long)g * a.units / G, u1 = (long)(g + 1) * a.units / G;
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsW = make_rsrc(a.Wt, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t rsO = make_rsrc(a.out, a.o_bytes), rsA = make_rsrc(a.add, a.o_bytes);
+  const int Wp = a.W + 2, Hp = a.H + 2, HW = a.H * a.W;
+  const int nc = a.Cr / 64, nsteps = 9 * nc;
+  const int kq = lane >> 4;
+  const long M = a.M;
+
+  // BN records [Ncols][G][HALO_WMW][3]: zero this workgroup's (the k-loop's
+  // vmcnt waits retire these stores before any record is written)
+  if (a.partial) {
+    for (int c = tid; c < a.Ncols * HALO_WMW; c += NT) {
+      float* rec = a.partial + ((long)(c / HALO_WMW) * G * HALO_WMW + (long)g * HALO_WMW + c % HALO_WMW) * 3;
+      rec[0] = rec[1] = rec[2] = 0.f;
+    }
+  }
+  if (u0 >= u1) return;
+
+  // a tile: column block cb, output pixels [m0, m0 + rows)
+  auto tile_rows = [&](long u, int& cb, int& m0) {
+    cb = (int)(u / M);
+    m0 = (int)(u - (long)cb * M);
+    const long end = min(u1, (long)(cb + 1) * M);
+    return (int)min((long)HB_TM, end - u);
+  };
+  auto issue_x = [&](int pr_lo, int npx, int cc, char* Xs) {
+    for (int i = wave; i * 8 < npx; i += NW) {
+      const int px = i * 8 + (lane >> 3);
+      const int rr = px / Wp, pc = px - rr * Wp;
+      const int pr = pr_lo + rr;
+      const int n = pr / Hp, ip = pr - n * Hp - 1, iw = pc - 1;
+      const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
+      const bool ok = px < npx && ip >= 0 && ip < a.H && iw >= 0 && iw < a.W;
+      const uint32_t off = (uint32_t)(((((long)n * a.H + ip) * a.W + iw) * a.Cr + cc * 64 + ch * 8) * 2);
+      blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
+    }
+  };
+  auto issue_b = [&](int cb, int ks, char* Bs) {
+    const int cc = ks / 9, t = ks - cc * 9;
+#pragma unroll
+    for (int l = 0; l < LB; ++l) {
+      const int i = wave + NW * l;
+      const int row = 8 * i + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);  // ktile_off's swizzle
+      const uint32_t off = (uint32_t)(((((long)cb * BN + row) * 9 + t) * a.Cr + cc * 64 + c * 8) * 2);
+      blds16(rsW, off, Bs + i * 1024);
+    }
+  };
+
+  int boff[FN][2];
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) boff[jj][kh] = ktile_off(wn * WTN + jj * 16 + (lane & 15), 4 * kh + kq);
+  const int rbase = wm * WTM + kq * 4, cbase = wn * WTN + (lane & 15);
+
+  WaveStats<FM, FN> ws;
+  ws.reset();
+
+  long u = u0;
+  int cb, m0;
+  int rows = tile_rows(u, cb, m0);
+  int pr_lo, npx;
+  hb_window(a, m0, rows, pr_lo, npx);
+  int xb = 0, sb = 0;
+  issue_x(pr_lo, npx, 0, smem + 2 * B_BYTES);
+  issue_b(cb, 0, smem);
+  for (;;) {
+    // this tile's A-row LDS pixels (tap (0, 0)) and output rows
+    int pxb[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * WTM + i * 16 + (lane & 15);
+      const int m = m0 + min(r, rows - 1);
+      const int n = m / HW, rem = m - n * HW, p = rem / a.W, q = rem - p * a.W;
+      pxb[i] = (n * Hp + p - pr_lo) * Wp + q;
+    }
+    const bool wact = wm * WTM < rows;  // the wave has rows in this tile (uniform)
+    // the next tile (its window is issued during this tile's last chunk)
+    const long un = u + rows;
+    const bool more = un < u1;
+    int cbn = cb, m0n = m0, rowsn = 0, pr_lon = 0, npxn = 0;
+    if (more) {
+      rowsn = tile_rows(un, cbn, m0n);
+      hb_window(a, m0n, rowsn, pr_lon, npxn);
+    }
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < nsteps; ++ks) {
+      wait_vm_barrier<0>();
+      const int cc = ks / 9, t = ks - cc * 9;
+      char* const Bs = smem + sb * B_BYTES;
+      char* const Xs = smem + 2 * B_BYTES + xb * HB_XBUF;
+      // prefetch: the next k-step's weights; at a chunk's first k-step the
+      // next chunk's window (the buffer the previous chunk was read from)
+      if (ks + 1 < nsteps) issue_b(cb, ks + 1, smem + (sb ^ 1) * B_BYTES);
+      else if (more) issue_b(cbn, 0, smem + (sb ^ 1) * B_BYTES);
+      if (t == 0) {
+        char* const Xn = smem + 2 * B_BYTES + (xb ^ 1) * HB_XBUF;
+        if (cc + 1 < nc) issue_x(pr_lo, npx, cc + 1, Xn);
+        else if (more) issue_x(pr_lon, npxn, 0, Xn);
+      }
+      if (wact && a.dbg != 1) {
+        const int tt = a.flip ? 8 - t : t;
+        const int toff = (tt / 3) * Wp + (tt - (tt / 3) * 3);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          Frag<T> fa[FM], fb[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            fa[i].v = *reinterpret_cast<const bf16x8*>(Xs + xtile_off(pxb[i] + toff, 4 * h + kq));
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj) fb[jj].v = *reinterpret_cast<const bf16x8*>(Bs + boff[jj][h]);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[i], fb[jj]);
+        }
+      }
+      sb ^= 1;
+      if (t == 8) xb ^= 1;
+    }
+
+    // ---- epilogue: 16-bit stores from the accumulators
+    uint32_t rowoff[FM][4];
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = rbase + i * 16 + e;
+        const bool v = r < rows;
+        rowoff[i][e] = v ? (uint32_t)((((long)(m0 + r)) * a.Ncols + cb * BN + cbase) * 2) : 0x80000000u;
+        vmask |= (v ? 1u : 0u) << (i * 4 + e);
+      }
+    if (a.partial && wact) ws.tile(acc, vmask);
+    if (a.add) {
+      short r[FM][FN][4];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[i][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsA, rowoff[i][e] + jj * 32, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = to_f32(from_f32<T>(acc[i][jj][e])) + to_f32(__builtin_bit_cast(T, r[i][jj][e]));
+            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(v)), rsO,
+                                                  rowoff[i][e] + jj * 32, 0, 0);
+          }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(acc[i][jj][e])), rsO,
+                                                  rowoff[i][e] + jj * 32, 0, 0);
+    }
+    // BN records of the column block when it ends (range end or block change)
+    if (a.partial && (!more || cbn != cb)) {
+      float n, mean[FN], m2[FN];
+      ws.wave_merge(n, mean, m2);
+      if (lane < 16) {
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj) {
+          const int c = cb * BN + cbase + jj * 16;
+          float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
+          rec[0] = n;
+          rec[1] = mean[jj] * n;
+          rec[2] = m2[jj];
+        }
+      }
+      ws.reset();
+    }
+    if (!more) break;
+    u = un; cb = cbn; m0 = m0n; rows = rowsn; pr_lo = pr_lon; npx = npxn;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // The stem conv (7x7 / stride 2 over the pre-padded 4-channel image, pad 0,
 // S padded to 8) in the same persistent, LDS-resident form.  A tile is
 // STEM_TR = 2 output rows; their 9 input rows (2 p0 .. 2 p0 + 8) are one
@@ -3465,6 +3723,72 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   return ::ssip::check_launch("conv_halo");
 }
 
+// ---- row-balanced halo path (conv_hb_kernel): 3x3 / stride 1 / pad 1, bf16,
+// >= 128 reduction channels (multiple of 64), output channels a multiple of
+// the column block.  SSIP_HB=0 turns it off; an SSIP_CONV_FORCE for the pass
+// selects the implicit-GEMM kernels instead.
+struct HbPlan {
+  int BN, G, cols, redc;
+  long units;
+};
+
+static bool hb_plan(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
+  const char* e = getenv("SSIP_HB");
+  if (!e || e[0] != '1') return false;  // opt-in while it is measured
+  const char* f = getenv("SSIP_CONV_FORCE");
+  if (f && f[0] == (mode == MODE_FWD ? 'f' : 'd')) return false;
+  if (dtype != SSIP_BF16 || !desc_ok(d) || d->R != 3 || d->S != 3 || d->stride != 1 || d->pad != 1 ||
+      d->P != d->H || d->Q != d->W)
+    return false;
+  const int redc = mode == MODE_FWD ? d->C : d->K;
+  const int cols = mode == MODE_FWD ? d->K : d->C;
+  const int BN = 128;
+  if (redc < 128 || redc % 64 != 0 || cols % BN != 0) return false;
+  const long M = (long)d->N * d->H * d->W;
+  if (M * redc * 2 >= (1l << 31) || M * cols * 2 >= (1l << 31) || (long)cols * 9 * redc * 2 >= (1l << 31))
+    return false;
+  hp.BN = BN;
+  hp.cols = cols;
+  hp.redc = redc;
+  hp.units = M * (cols / BN);
+  hp.G = (int)std::min<long>(device_cus(), (hp.units + 63) / 64);
+  // every tile's input window must fit one LDS buffer (hb_window)
+  const int HW = d->H * d->W, Hp = d->H + 2, Wp = d->W + 2;
+  for (int g = 0; g < hp.G; ++g) {
+    const long u0 = (long)g * hp.units / hp.G, u1 = (long)(g + 1) * hp.units / hp.G;
+    for (long u = u0; u < u1;) {
+      const long cb = u / M, m0 = u - cb * M;
+      const long rows = std::min<long>(HB_TM, std::min(u1, (cb + 1) * M) - u);
+      const long m1 = m0 + rows - 1;
+      const long n0 = m0 / HW, p0 = (m0 - n0 * HW) / d->W, n1 = m1 / HW, p1 = (m1 - n1 * HW) / d->W;
+      if ((n1 * Hp + p1 + 3 - (n0 * Hp + p0)) * Wp > HB_XBUF / 128) return false;
+      u += rows;
+    }
+  }
+  return true;
+}
+
+static int launch_hb(int mode, const ssip_conv_desc* d, const HbPlan& hp, const void* X, const void* Wt, void* out,
+                     const void* add, float* partial, hipStream_t st) {
+  HbArgs h;
+  memset(&h, 0, sizeof(h));
+  h.X = static_cast<const __bf16*>(X);
+  h.Wt = static_cast<const __bf16*>(Wt);
+  h.out = static_cast<__bf16*>(out);
+  h.add = static_cast<const __bf16*>(add);
+  h.partial = partial;
+  const long M = (long)d->N * d->H * d->W;
+  h.x_bytes = (uint32_t)(M * hp.redc * 2);
+  h.w_bytes = (uint32_t)((long)hp.cols * 9 * hp.redc * 2);
+  h.o_bytes = (uint32_t)(M * hp.cols * 2);
+  h.N = d->N; h.H = d->H; h.W = d->W; h.Cr = hp.redc; h.Ncols = hp.cols; h.M = (int)M;
+  h.flip = mode == MODE_DGRAD ? 1 : 0;
+  h.units = hp.units;
+  { const char* dbg = getenv("SSIP_HB_DBG"); h.dbg = dbg ? atoi(dbg) : 0; }
+  hipLaunchKernelGGL((conv_hb_kernel<128, 2>), dim3(hp.G), dim3(512), 0, st, h);
+  return ::ssip::check_launch("conv_hb");
+}
+
 }  // namespace
 
 extern "C" {
@@ -3479,6 +3803,8 @@ int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d) {
   HaloPlan hp;  // one record per (channel, workgroup) on the halo path
   if (halo_plan(MODE_FWD, d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
   if (stem_plan(d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
+  HbPlan hb;
+  if (hb_plan(MODE_FWD, d, SSIP_BF16, hb)) n = std::max(n, (int64_t)hb.G * HALO_WMW * d->K * 3);
   // + the scratch of ssip_bn_finalize's split pass (the most records any
   // plan writes bounds the splits; the scratch starts behind the records)
   return n + fin_scratch_floats(d->K, n / (3 * d->K), 3);
@@ -3495,6 +3821,9 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
   if (halo_plan(MODE_FWD, d, dtype, hp))
     return launch_halo(MODE_FWD, d, hp, x, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream);
   if (stem_plan(d, dtype, hp)) return launch_stem_halo(d, hp, x, w_krsc, y, bn_partial, (hipStream_t)stream);
+  HbPlan hb;
+  if (hb_plan(MODE_FWD, d, dtype, hb))
+    return launch_hb(MODE_FWD, d, hb, x, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream);
   pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
@@ -3512,6 +3841,8 @@ static bool fwd_ds_plan(const ssip_conv_desc* d, const ssip_conv_desc* dds, int 
     return false;
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp) || stem_plan(d, dtype, hp)) return false;
+  HbPlan hb;
+  if (hb_plan(MODE_FWD, d, dtype, hb)) return false;
   if (plan_conv(MODE_FWD, d, 2, pl) != SSIP_OK || pl.conv1) return false;
   return pl.stages == 2 || pl.stages == 3;
 }
@@ -3550,6 +3881,8 @@ int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp)) return hp.G * HALO_WMW;
   if (stem_plan(d, dtype, hp)) return hp.G * HALO_WMW;
+  HbPlan hb;
+  if (hb_plan(MODE_FWD, d, dtype, hb)) return hb.G * HALO_WMW;
   Plan pl;
   if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
   if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
@@ -3585,6 +3918,9 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   HaloPlan hp;
   if (halo_plan(MODE_DGRAD, d, dtype, hp))
     return launch_halo(MODE_DGRAD, d, hp, dy, w_crsk, dx, dx_add, nullptr, (hipStream_t)stream);
+  HbPlan hb;
+  if (hb_plan(MODE_DGRAD, d, dtype, hb))
+    return launch_hb(MODE_DGRAD, d, hb, dy, w_crsk, dx, dx_add, nullptr, (hipStream_t)stream);
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
@@ -3859,6 +4195,11 @@ int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* bu
   }
   if (m == MODE_DGRAD && halo_plan(MODE_DGRAD, d, dtype, hp)) {
     snprintf(buf, buflen, "halo<dgrad,TR=%d,G=%d>", hp.TR, hp.G);
+    return SSIP_OK;
+  }
+  HbPlan hb;
+  if ((m == MODE_FWD || m == MODE_DGRAD) && hb_plan(m, d, dtype, hb)) {
+    snprintf(buf, buflen, "hb<%s,%d,G=%d>", mname[mode], hb.BN, hb.G);
     return SSIP_OK;
   }
   if (m == MODE_WGRAD && stem_wg_plan(d, dtype, hp)) {

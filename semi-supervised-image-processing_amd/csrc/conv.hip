@@ -2210,45 +2210,57 @@ struct HbArgs {
   const __bf16* add;  // DGRAD residual gradient (nullable, may alias out)
   float* partial;     // FWD BN records (nullable)
   uint32_t x_bytes, w_bytes, o_bytes;
-  int N, H, W, Cr, Ncols, M, flip;
+  int N, H, W, Cr, Ncols, M;
+  int lxw;            // log2 of the LDS image's row pitch XW >= W + 2 (pixels)
+  FastDiv div_hp;     // / (H + 2)
   long units;         // M * (Ncols / BN)
-  int dbg;            // timing ablations (tools): 1 = no MFMA
+  int tm;             // output pixels per tile (<= HB_TM; the host's choice keeps every window in HB_XBUF)
+  int dbg;            // timing ablations (tools): 1 = no MFMA, 2 = every wave multiplies all its fragments
 };
 
-constexpr int HB_XBUF = 52 * 1024;  // one input window: <= 416 pixels x 128 B (host-checked)
+constexpr int HB_XBUF = 56 * 1024;  // one input window: <= 448 pixels x 128 B (host-checked)
 constexpr int HB_TM = 256;          // output pixels per tile
 
 // input window of the tile [m0, m0 + rows): padded rows n (H+2) + p + 1 of
 // input row p = -1 .. H of image n, from the first output row's p - 1 to the
-// last one's p + 1
+// last one's p + 1; LDS rows of XW = 2^lxw pixels (a power of two >= W + 2, so
+// a tap's row shift r XW keeps every pixel's swizzle phase)
 __device__ __forceinline__ void hb_window(const HbArgs& a, int m0, int rows, int& pr_lo, int& npx) {
   const int HW = a.H * a.W, Hp = a.H + 2;
   const int n0 = m0 / HW, p0 = (m0 - n0 * HW) / a.W;
   const int m1 = m0 + rows - 1;
   const int n1 = m1 / HW, p1 = (m1 - n1 * HW) / a.W;
   pr_lo = n0 * Hp + p0;
-  npx = min((n1 * Hp + p1 + 3 - pr_lo) * (a.W + 2), HB_XBUF / 128);
+  npx = min((n1 * Hp + p1 + 3 - pr_lo) << a.lxw, HB_XBUF / 128);
 }
 
-template <int BN, int WNW>
+template <int BN, int WNW, bool FLIP>
 __global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
   typedef __bf16 T;
   constexpr int WMW = 4, NW = WMW * WNW, NT = 64 * NW;
   constexpr int WTM = HB_TM / WMW, WTN = BN / WNW, FM = WTM / 16, FN = WTN / 16;
   constexpr int B_BYTES = BN * 128;
-  constexpr int IB = B_BYTES / 1024, LB = IB / NW;  // weight DMA instructions per k-step / per wave
-  static_assert(IB % NW == 0 && LB >= 1 && FM == 4 && FN >= 1 && WMW <= HALO_WMW, "hb tile");
-  __shared__ __attribute__((aligned(16))) char smem[2 * B_BYTES + 2 * HB_XBUF];
+  constexpr int NWI = NW;  // every wave issues its share of the LDS-DMA
+  constexpr int IB = B_BYTES / 1024, LB = IB / NWI;  // weight DMA instructions per k-step / per issuing wave
+  constexpr int NXW = HB_XBUF / 1024 / NWI;          // window DMA instructions per chunk / per issuing wave (fixed)
+  constexpr int NSB = 3;                             // weight ring: k-steps ks+1, ks+2 in flight during ks
+  static_assert(IB % NWI == 0 && LB >= 1 && FM == 4 && FN >= 1 && WMW <= HALO_WMW && HB_XBUF % (1024 * NWI) == 0,
+                "hb tile");
+  static_assert(NSB * B_BYTES + 2 * HB_XBUF <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NSB * B_BYTES + 2 * HB_XBUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WNW, wn = wave % WNW;
+  // waves w and w + 4 share a SIMD: pair wave rows (0, 3) and (1, 2), so a
+  // ragged tile (rows filling wave rows 0, 1, ... in order) loads the SIMDs evenly
+  static_assert(WNW == 2, "the SIMD pairing below assumes 4 x 2 waves");
+  const int wm = wave < 4 ? (wave >> 1) : 3 - ((wave - 4) >> 1), wn = wave & 1;
   const int G = gridDim.x, g = blockIdx.x;
   const long u0 = (long)g * a.units / G, u1 = (long)(g + 1) * a.units / G;
   const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsW = make_rsrc(a.Wt, a.w_bytes);
   const __amdgpu_buffer_rsrc_t rsO = make_rsrc(a.out, a.o_bytes), rsA = make_rsrc(a.add, a.o_bytes);
-  const int Wp = a.W + 2, Hp = a.H + 2, HW = a.H * a.W;
-  const int nc = a.Cr / 64, nsteps = 9 * nc;
+  const int Hp = a.H + 2, HW = a.H * a.W, XW = 1 << a.lxw;
+  const int nc = a.Cr / 64;
   const int kq = lane >> 4;
   const long M = a.M;
 
@@ -2267,30 +2279,37 @@ __global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
     cb = (int)(u / M);
     m0 = (int)(u - (long)cb * M);
     const long end = min(u1, (long)(cb + 1) * M);
-    return (int)min((long)HB_TM, end - u);
+    return (int)min((long)a.tm, end - u);
   };
+  // always NXW instructions per wave (pixels past the window read zeros), so
+  // the counted vmcnt waits below see a fixed number of younger operations
   auto issue_x = [&](int pr_lo, int npx, int cc, char* Xs) {
-    for (int i = wave; i * 8 < npx; i += NW) {
+#pragma unroll 1
+    for (int k = 0; k < NXW; ++k) {
+      const int i = wave + NWI * k;
       const int px = i * 8 + (lane >> 3);
-      const int rr = px / Wp, pc = px - rr * Wp;
-      const int pr = pr_lo + rr;
-      const int n = pr / Hp, ip = pr - n * Hp - 1, iw = pc - 1;
+      const int pr = pr_lo + (px >> a.lxw), pc = px & (XW - 1);
+      const int n = (int)fdiv((uint32_t)pr, a.div_hp), ip = pr - n * Hp - 1, iw = pc - 1;
       const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
-      const bool ok = px < npx && ip >= 0 && ip < a.H && iw >= 0 && iw < a.W;
+      const bool ok = px < npx && (uint32_t)ip < (uint32_t)a.H && (uint32_t)iw < (uint32_t)a.W;
       const uint32_t off = (uint32_t)(((((long)n * a.H + ip) * a.W + iw) * a.Cr + cc * 64 + ch * 8) * 2);
       blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
     }
   };
-  auto issue_b = [&](int cb, int ks, char* Bs) {
-    const int cc = ks / 9, t = ks - cc * 9;
+  // weight rows of the column block: per lane its rows' byte offsets at tap 0, chunk 0
+  uint32_t woff[LB];
+  auto set_woff = [&](int cb) {
 #pragma unroll
     for (int l = 0; l < LB; ++l) {
-      const int i = wave + NW * l;
-      const int row = 8 * i + (lane >> 3);
+      const int row = 8 * (wave + NWI * l) + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);  // ktile_off's swizzle
-      const uint32_t off = (uint32_t)(((((long)cb * BN + row) * 9 + t) * a.Cr + cc * 64 + c * 8) * 2);
-      blds16(rsW, off, Bs + i * 1024);
+      woff[l] = (uint32_t)((((long)cb * BN + row) * 9 * a.Cr + c * 8) * 2);
     }
+  };
+  auto issue_b = [&](int cc, int t, char* Bs) {
+    const uint32_t k = (uint32_t)((t * a.Cr + cc * 64) * 2);
+#pragma unroll
+    for (int l = 0; l < LB; ++l) blds16(rsW, woff[l] + k, Bs + (wave + NWI * l) * 1024);
   };
 
   int boff[FN][2];
@@ -2308,18 +2327,27 @@ __global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
   int rows = tile_rows(u, cb, m0);
   int pr_lo, npx;
   hb_window(a, m0, rows, pr_lo, npx);
-  int xb = 0, sb = 0;
-  issue_x(pr_lo, npx, 0, smem + 2 * B_BYTES);
-  issue_b(cb, 0, smem);
+  char* const Xbuf = smem + NSB * B_BYTES;
+  const bool g1 = wave >= 4;  // group 1: waves 4-7, one beside each group-0 wave on its SIMD
+  set_woff(cb);
+  issue_x(pr_lo, npx, 0, Xbuf);
+  issue_b(0, 0, smem);
+  issue_b(0, 1, smem + B_BYTES);
+  int xb = 0, sb = 0;  // window buffer of the current chunk, weight stage of the current k-step
   for (;;) {
-    // this tile's A-row LDS pixels (tap (0, 0)) and output rows
-    int pxb[FM];
+    // this tile's A-fragment LDS addresses for each column shift s of a tap
+    // (the row shift r XW * 128 B is added per k-step)
+    // (k-half 1's slot is k-half 0's with bit 2 flipped: address ^ 64, which
+    // commutes with the row shift, a multiple of 2 KiB)
+    int abase[FM][3];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int r = wm * WTM + i * 16 + (lane & 15);
       const int m = m0 + min(r, rows - 1);
       const int n = m / HW, rem = m - n * HW, p = rem / a.W, q = rem - p * a.W;
-      pxb[i] = (n * Hp + p - pr_lo) * Wp + q;
+      const int pxb = ((n * Hp + p - pr_lo) << a.lxw) + q;
+#pragma unroll
+      for (int s3 = 0; s3 < 3; ++s3) abase[i][s3] = xtile_off(pxb + s3, kq);
     }
     const bool wact = wm * WTM < rows;  // the wave has rows in this tile (uniform)
     // the next tile (its window is issued during this tile's last chunk)
@@ -2335,40 +2363,98 @@ __global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < nsteps; ++ks) {
-      wait_vm_barrier<0>();
-      const int cc = ks / 9, t = ks - cc * 9;
-      char* const Bs = smem + sb * B_BYTES;
-      char* const Xs = smem + 2 * B_BYTES + xb * HB_XBUF;
-      // prefetch: the next k-step's weights; at a chunk's first k-step the
-      // next chunk's window (the buffer the previous chunk was read from)
-      if (ks + 1 < nsteps) issue_b(cb, ks + 1, smem + (sb ^ 1) * B_BYTES);
-      else if (more) issue_b(cbn, 0, smem + (sb ^ 1) * B_BYTES);
-      if (t == 0) {
-        char* const Xn = smem + 2 * B_BYTES + (xb ^ 1) * HB_XBUF;
-        if (cc + 1 < nc) issue_x(pr_lo, npx, cc + 1, Xn);
-        else if (more) issue_x(pr_lon, npxn, 0, Xn);
-      }
-      if (wact && a.dbg != 1) {
-        const int tt = a.flip ? 8 - t : t;
-        const int toff = (tt / 3) * Wp + (tt - (tt / 3) * 3);
+    // The tile's k-loop as a two-group ping-pong (MI355X_MICROARCH.md, "Two
+    // waves per SIMD"): every wave runs read(s) | mfma(s) | read(s+1) | ...
+    // with a barrier at each "|", and group 1 (waves 4-7) passes one extra
+    // barrier first, so on every SIMD one wave multiplies while its partner
+    // reads fragments and issues its share of the LDS-DMA (weights of k-step
+    // s + 2; at a chunk's second k-step the next chunk's window).  After its
+    // reads a wave retires them (lgkmcnt(0): the stage they read may be
+    // refilled after the next barrier) and, with a counted vmcnt, its share
+    // of k-step s + 1's weights (read after the barrier after next).
+    // NF = this wave's valid row fragments (uniform): fragments past the
+    // tile's rows are neither read nor multiplied.
+    auto kloop = [&](auto nfc) {
+      constexpr int NF = decltype(nfc)::value;
+      bool switched = false;  // woff moved on to the next tile's column block
+      auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      // everything this tile's first k-step reads has landed (and the previous
+      // tile's epilogue stores have retired)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (g1) bar();
+      for (int cc = 0; cc < nc; ++cc) {
+        char* const Xs = Xbuf + xb * HB_XBUF;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          Frag<T> fa[FM], fb[FN];
+        for (int t = 0; t < 9; ++t) {
+          char* const Bs = smem + sb * B_BYTES;
+          // ---- read(s) + this wave's DMA share
+          bar();
+          Frag<T> fa[2][FM], fb[2][FN];
+          if (NF > 0 && a.dbg != 1) {
+            // DGRAD: weight tap t reads dy at the flipped shift 8 - t
+            const int tt = FLIP ? 8 - t : t;
+            const int rr = tt / 3, s3 = tt % 3;
+            const int roff = (rr << a.lxw) * 128;
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
-            fa[i].v = *reinterpret_cast<const bf16x8*>(Xs + xtile_off(pxb[i] + toff, 4 * h + kq));
+            for (int h = 0; h < 2; ++h) {
 #pragma unroll
-          for (int jj = 0; jj < FN; ++jj) fb[jj].v = *reinterpret_cast<const bf16x8*>(Bs + boff[jj][h]);
+              for (int i = 0; i < NF; ++i)
+                fa[h][i].v = *reinterpret_cast<const bf16x8*>(Xs + ((abase[i][s3] + roff) ^ (h << 6)));
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
+              for (int jj = 0; jj < FN; ++jj) fb[h][jj].v = *reinterpret_cast<const bf16x8*>(Bs + boff[jj][h]);
+            }
+          }
+          {
+            // weights of k-step s + 2 into the stage k-step s - 1 was read from
+            const int sb2 = sb == 0 ? 2 : sb - 1;
+            const int t2 = t + 2 < 9 ? t + 2 : t - 7;
+            int cc2 = t + 2 < 9 ? cc : cc + 1;
+            if (cc2 >= nc) {  // the next tile's k-steps (or, with none left, a dummy that keeps the count)
+              if (more && !switched && cbn != cb) set_woff(cbn);
+              switched = true;
+              cc2 = 0;
+            }
+            issue_b(cc2, more || cc2 > 0 || t + 2 < 9 ? t2 : 0, smem + sb2 * B_BYTES);
+            // the next chunk's window into the buffer the previous chunk was
+            // read from (both groups finished it before this k-step)
+            if (t == 1) {
+              const bool same = cc + 1 < nc;
+              issue_x(same ? pr_lo : pr_lon, same ? npx : (more ? npxn : 0), same ? cc + 1 : 0,
+                      Xbuf + (xb ^ 1) * HB_XBUF);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          // younger than k-step s + 1's weights: k-step s + 2's and the window
+          // instructions of k-steps with t == 1 (this one or the previous one)
+          if (t == 1 || t == 2) asm volatile("s_waitcnt lgkmcnt(0) vmcnt(%0)" ::"n"(LB + NXW) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0) vmcnt(%0)" ::"n"(LB) : "memory");
+          // ---- mfma(s)
+          bar();
+          if (NF > 0 && a.dbg != 1) {
 #pragma unroll
-            for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[i], fb[jj]);
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int i = 0; i < NF; ++i)
+#pragma unroll
+                for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[h][i], fb[h][jj]);
+          }
+          sb = sb == NSB - 1 ? 0 : sb + 1;
         }
+        xb ^= 1;
       }
-      sb ^= 1;
-      if (t == 8) xb ^= 1;
-    }
+      if (!g1) bar();
+    };
+    const int nf = wact ? (a.dbg == 2 ? FM : min(FM, (rows - wm * WTM + 15) >> 4)) : 0;
+    static_assert(FM == 4, "kloop dispatch");
+    if (nf == 4) kloop(std::integral_constant<int, 4>());
+    else if (nf == 3) kloop(std::integral_constant<int, 3>());
+    else if (nf == 2) kloop(std::integral_constant<int, 2>());
+    else if (nf == 1) kloop(std::integral_constant<int, 1>());
+    else kloop(std::integral_constant<int, 0>());
 
     // ---- epilogue: 16-bit stores from the accumulators
     uint32_t rowoff[FM][4];
@@ -2430,6 +2516,8 @@ __global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
     if (!more) break;
     u = un; cb = cbn; m0 = m0n; rows = rowsn; pr_lo = pr_lon; npx = npxn;
   }
+  // the dummy prefetches land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -3728,15 +3816,48 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
 // the column block.  SSIP_HB=0 turns it off; an SSIP_CONV_FORCE for the pass
 // selects the implicit-GEMM kernels instead.
 struct HbPlan {
-  int BN, G, cols, redc;
+  int BN, G, cols, redc, lxw, tm;
   long units;
 };
 
+static bool hb_plan_compute(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp);
+
+// hb_plan_compute's tile search walks every workgroup's tiles: cached per
+// geometry (per thread), so a launch costs the host a lookup
 static bool hb_plan(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
+  // SSIP_HB=0: never; =1: wherever the kernel applies; default: where it
+  // measured faster than the implicit-GEMM kernels (tools/time_hb.py):
+  // LDS rows at least 3/4 filled (W + 2 >= 3/4 of the power-of-two pitch) and
+  // full 256-pixel tiles
   const char* e = getenv("SSIP_HB");
-  if (!e || e[0] != '1') return false;  // opt-in while it is measured
+  const int force = e && e[0] == '1' ? 1 : (e && e[0] == '0' ? 0 : -1);
+  if (force == 0) return false;
   const char* f = getenv("SSIP_CONV_FORCE");
   if (f && f[0] == (mode == MODE_FWD ? 'f' : 'd')) return false;
+  struct Entry {
+    int key[12];
+    bool ok;
+    HbPlan hp;
+  };
+  static thread_local Entry cache[32];
+  static thread_local int ncache = 0, next = 0;
+  const int key[12] = {mode, dtype, d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->pad, device_cus()};
+  for (int i = 0; i < ncache; ++i)
+    if (memcmp(cache[i].key, key, sizeof(key)) == 0) {
+      hp = cache[i].hp;
+      return cache[i].ok;
+    }
+  Entry& en = cache[next];
+  next = (next + 1) % 32;
+  ncache = std::min(ncache + 1, 32);
+  memcpy(en.key, key, sizeof(key));
+  en.ok = hb_plan_compute(mode, d, dtype, en.hp);
+  hp = en.hp;
+  if (!en.ok) return false;
+  return force == 1 || (4 * (d->W + 2) >= 3 * (1 << hp.lxw) && hp.tm == HB_TM);
+}
+
+static bool hb_plan_compute(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
   if (dtype != SSIP_BF16 || !desc_ok(d) || d->R != 3 || d->S != 3 || d->stride != 1 || d->pad != 1 ||
       d->P != d->H || d->Q != d->W)
     return false;
@@ -3752,19 +3873,41 @@ static bool hb_plan(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
   hp.redc = redc;
   hp.units = M * (cols / BN);
   hp.G = (int)std::min<long>(device_cus(), (hp.units + 63) / 64);
-  // every tile's input window must fit one LDS buffer (hb_window)
-  const int HW = d->H * d->W, Hp = d->H + 2, Wp = d->W + 2;
-  for (int g = 0; g < hp.G; ++g) {
-    const long u0 = (long)g * hp.units / hp.G, u1 = (long)(g + 1) * hp.units / hp.G;
-    for (long u = u0; u < u1;) {
-      const long cb = u / M, m0 = u - cb * M;
-      const long rows = std::min<long>(HB_TM, std::min(u1, (cb + 1) * M) - u);
-      const long m1 = m0 + rows - 1;
-      const long n0 = m0 / HW, p0 = (m0 - n0 * HW) / d->W, n1 = m1 / HW, p1 = (m1 - n1 * HW) / d->W;
-      if ((n1 * Hp + p1 + 3 - (n0 * Hp + p0)) * Wp > HB_XBUF / 128) return false;
-      u += rows;
+  // tile size: every tile's input window must fit one LDS buffer (hb_window);
+  // among those, the one whose slowest workgroup has the least MFMA work per
+  // SIMD (conv_hb_kernel pairs wave rows (0, 3) and (1, 2) on a SIMD and skips
+  // fragments past a tile's rows), plus one fragment's worth per tile for its
+  // prologue and epilogue
+  int lxw = 0;
+  while ((1 << lxw) < d->W + 2) ++lxw;
+  hp.lxw = lxw;
+  const int HW = d->H * d->W, Hp = d->H + 2, Wp = 1 << lxw;
+  hp.tm = 0;
+  long best = -1;
+  auto nfr = [](long rows, int wr) { return (int)std::max<long>(0, std::min<long>(4, (rows - 64 * wr + 15) / 16)); };
+  for (int tm = HB_TM; tm >= 32; tm -= 16) {
+    bool fits = true;
+    long worst = 0;
+    for (int g = 0; g < hp.G && fits; ++g) {
+      const long u0 = (long)g * hp.units / hp.G, u1 = (long)(g + 1) * hp.units / hp.G;
+      long cost = 0;
+      for (long u = u0; u < u1 && fits;) {
+        const long cb = u / M, m0 = u - cb * M;
+        const long rows = std::min<long>(tm, std::min(u1, (cb + 1) * M) - u);
+        const long m1 = m0 + rows - 1;
+        const long n0 = m0 / HW, p0 = (m0 - n0 * HW) / d->W, n1 = m1 / HW, p1 = (m1 - n1 * HW) / d->W;
+        fits = (n1 * Hp + p1 + 3 - (n0 * Hp + p0)) * Wp <= HB_XBUF / 128;
+        cost += std::max(nfr(rows, 0) + nfr(rows, 3), nfr(rows, 1) + nfr(rows, 2)) + 1;
+        u += rows;
+      }
+      worst = std::max(worst, cost);
+    }
+    if (fits && (best < 0 || worst < best)) {
+      best = worst;
+      hp.tm = tm;
     }
   }
+  if (hp.tm == 0) return false;
   return true;
 }
 
@@ -3782,10 +3925,15 @@ static int launch_hb(int mode, const ssip_conv_desc* d, const HbPlan& hp, const 
   h.w_bytes = (uint32_t)((long)hp.cols * 9 * hp.redc * 2);
   h.o_bytes = (uint32_t)(M * hp.cols * 2);
   h.N = d->N; h.H = d->H; h.W = d->W; h.Cr = hp.redc; h.Ncols = hp.cols; h.M = (int)M;
-  h.flip = mode == MODE_DGRAD ? 1 : 0;
+  h.lxw = hp.lxw;
+  h.div_hp = make_fastdiv((uint32_t)(d->H + 2));
   h.units = hp.units;
+  h.tm = hp.tm;
   { const char* dbg = getenv("SSIP_HB_DBG"); h.dbg = dbg ? atoi(dbg) : 0; }
-  hipLaunchKernelGGL((conv_hb_kernel<128, 2>), dim3(hp.G), dim3(512), 0, st, h);
+  if (mode == MODE_DGRAD)
+    hipLaunchKernelGGL((conv_hb_kernel<128, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
+  else
+    hipLaunchKernelGGL((conv_hb_kernel<128, 2, false>), dim3(hp.G), dim3(512), 0, st, h);
   return ::ssip::check_launch("conv_hb");
 }
 
@@ -4199,7 +4347,7 @@ int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* bu
   }
   HbPlan hb;
   if ((m == MODE_FWD || m == MODE_DGRAD) && hb_plan(m, d, dtype, hb)) {
-    snprintf(buf, buflen, "hb<%s,%d,G=%d>", mname[mode], hb.BN, hb.G);
+    snprintf(buf, buflen, "hb<%s,%d,TM=%d,G=%d>", mname[mode], hb.BN, hb.tm, hb.G);
     return SSIP_OK;
   }
   if (m == MODE_WGRAD && stem_wg_plan(d, dtype, hp)) {

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="l2.3x3,l3.3x3,l4.3x3")
+    ap.add_argument("--dbg", default="", help="comma-separated SSIP_HB_DBG values timed as extra hb variants")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
@@ -36,16 +37,20 @@ def main():
             for mode, fn in (("f", lambda: ops.conv_fwd(g, x, w, y, part)), ("d", lambda: ops.conv_dgrad(g, dy, wc, dx))):
                 if batch == 128 and mode == "d":
                     continue
-                res = {"0": [], "1": []}
+                variants = ["0", "1"] + ["1d" + d for d in a.dbg.split(",") if d]
+                res = {v: [] for v in variants}
                 names = {}
                 for _ in range(a.rounds):
-                    for v in ("0", "1"):
-                        os.environ["SSIP_HB"] = v
+                    for v in variants:
+                        os.environ["SSIP_HB"] = v[0]
+                        os.environ["SSIP_HB_DBG"] = v[2:] if len(v) > 1 else "0"
                         names[v] = ops.conv_kernel_name("fwd" if mode == "f" else "dgrad", g, bf)
                         res[v].append(time_fn(fn, a.iters))
+                os.environ["SSIP_HB_DBG"] = "0"
                 t0, t1 = sorted(res["0"])[a.rounds // 2], sorted(res["1"])[a.rounds // 2]
                 print(f"bs{batch} {nm:7s} {mode}  default {t0:7.1f} us ({g.flops() / t0 / 1e6:5.0f} TF/s) {names['0']:28s}"
-                      f"  hb {t1:7.1f} us ({g.flops() / t1 / 1e6:5.0f} TF/s) {names['1']}", flush=True)
+                      f"  hb {t1:7.1f} us ({g.flops() / t1 / 1e6:5.0f} TF/s) {names['1']}" +
+                      "".join(f"  dbg{v[2:]} {sorted(res[v])[a.rounds // 2]:7.1f}" for v in variants[2:]), flush=True)
 
 
 if __name__ == "__main__":

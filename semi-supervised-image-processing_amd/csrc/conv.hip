@@ -3842,18 +3842,22 @@ static bool hb_plan(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
   static thread_local Entry cache[32];
   static thread_local int ncache = 0, next = 0;
   const int key[12] = {mode, dtype, d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->pad, device_cus()};
-  for (int i = 0; i < ncache; ++i)
-    if (memcmp(cache[i].key, key, sizeof(key)) == 0) {
-      hp = cache[i].hp;
-      return cache[i].ok;
-    }
-  Entry& en = cache[next];
-  next = (next + 1) % 32;
-  ncache = std::min(ncache + 1, 32);
-  memcpy(en.key, key, sizeof(key));
-  en.ok = hb_plan_compute(mode, d, dtype, en.hp);
-  hp = en.hp;
-  if (!en.ok) return false;
+  const Entry* hit = nullptr;
+  for (int i = 0; i < ncache && !hit; ++i)
+    if (memcmp(cache[i].key, key, sizeof(key)) == 0) hit = &cache[i];
+  if (!hit) {
+    Entry& en = cache[next];
+    next = (next + 1) % 32;
+    ncache = std::min(ncache + 1, 32);
+    memcpy(en.key, key, sizeof(key));
+    en.ok = hb_plan_compute(mode, d, dtype, en.hp);
+    hit = &en;
+  }
+  hp = hit->hp;
+  // the same answer on every call for this geometry and environment: the
+  // BN-record sizing (ssip_conv_fwd_partial_floats / _tiles) and the launch
+  // must agree
+  if (!hit->ok) return false;
   return force == 1 || (4 * (d->W + 2) >= 3 * (1 << hp.lxw) && hp.tm == HB_TM);
 }
 

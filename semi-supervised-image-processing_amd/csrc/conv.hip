@@ -3825,13 +3825,19 @@ static bool hb_plan_compute(int mode, const ssip_conv_desc* d, int dtype, HbPlan
 // hb_plan_compute's tile search walks every workgroup's tiles: cached per
 // geometry (per thread), so a launch costs the host a lookup
 static bool hb_plan(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
-  // SSIP_HB=0: never; =1: wherever the kernel applies; default: where it
-  // measured faster than the implicit-GEMM kernels (tools/time_hb.py):
-  // LDS rows at least 3/4 filled (W + 2 >= 3/4 of the power-of-two pitch) and
-  // full 256-pixel tiles
+  // Off by default: faster per launch where it applies (l2 / l3 3x3 at batch
+  // 256: -4..-10 %, tools/time_hb.py) but slower in the train step (6.59 vs
+  // 6.49 ms/step: a persistent workgroup holding a CU's whole LDS keeps the
+  // side streams' kernels off it; profiles/r3_hb.txt).  SSIP_HB=1: wherever
+  // the kernel applies; =2: where it measured faster per launch (LDS rows at
+  // least 3/4 filled -- W + 2 >= 3/4 of the power-of-two pitch -- and full
+  // 256-pixel tiles); =f / =d / =n: that rule for the forward / the dgrad /
+  // batches of 256+ only.
   const char* e = getenv("SSIP_HB");
-  const int force = e && e[0] == '1' ? 1 : (e && e[0] == '0' ? 0 : -1);
-  if (force == 0) return false;
+  if (!e || !e[0] || e[0] == '0') return false;
+  const int force = e[0] == '1' ? 1 : -1;
+  if (e && ((e[0] == 'f' && mode != MODE_FWD) || (e[0] == 'd' && mode != MODE_DGRAD))) return false;
+  if (e && e[0] == 'n' && d->N < 256) return false;  // =n: batches of 256+ only (the train pass, not the weak forward)
   const char* f = getenv("SSIP_CONV_FORCE");
   if (f && f[0] == (mode == MODE_FWD ? 'f' : 'd')) return false;
   struct Entry {

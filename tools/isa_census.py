@@ -1,4 +1,5 @@
-"""Instruction census of a kernel's main loop from hipcc device assembly.
+"""Instruction census of a kernel's main loop from hipcc device assembly
+(static counts: a branch's instructions count once per loop body).
 
 usage (host, no GPU):
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -munsafe-fp-atomics --cuda-device-only -S \
@@ -134,7 +135,11 @@ def main():
                 c, w = census(lines, s, e)
                 if c["mfma"] == 0:
                     continue
-                if best is None or c["mfma"] > best[0]["mfma"]:
+                # the k-loop: most MFMAs; among back edges to the same header
+                # (a rotated loop's continue paths), the widest span, so the
+                # conditionally issued loads are counted too
+                if best is None or c["mfma"] > best[0]["mfma"] or (
+                        c["mfma"] == best[0]["mfma"] and lab == best[2] and e - s > best[4] - best[3]):
                     best = (c, w, lab, s, e)
             if best is None:
                 print("   no MFMA loop")

@@ -3210,6 +3210,272 @@ __global__ void __launch_bounds__(512, 2) conv_stem_bwd_wgrad_kernel(const StemB
         }
 }
 
+// The same fused stem backward tail with the two halves specialised
+// (tools/time_stem_bw.py: DMA + sync alone 133 us, the dy pass +72, the
+// MFMAs +74, and the two do not overlap in conv_stem_bwd_wgrad_kernel, where
+// every wave runs both behind a barrier): waves 0-3 form dy, waves 4-7
+// multiply.  A tile's 224 GEMM rows are cut into half A (output columns
+// 0-63 of both rows: 128 rows, 4 k-steps) and half B (columns 64-111: 96
+// rows, 3 k-steps), GEMM row = 16 columns x 2 rows per 32-row chunk (the
+// 2x2 pixel blocks of 8 pooled windows).  Phase (u, A): the dy waves form
+// (u, B) while the MFMA waves run (u, A); phase (u, B): the dy waves form
+// (u+1, A) while the MFMA waves run (u, B); one barrier per phase, each half
+// in its own slot, so on every SIMD one wave's VALU work runs beside its
+// partner's MFMAs.  The input regions are refilled as soon as their last
+// reader is done, two phases ahead of their next reader: x of tile u+1 at
+// (u, A) (x of u-1 was last read at (u-1, B)); y, the pooled gradient and
+// the argmax of tile u+2 at (u, B) (those of u were last read at (u, A)).
+// The dy waves issue every LDS-DMA, a fixed count per wave per region, and
+// retire each region with a counted vmcnt before the barrier ahead of its
+// first reader.  Same dy formula and (p, q)-ascending window order as above;
+// the MFMA k-order within a tile differs (column chunks), so results agree
+// to fp32 rounding.
+constexpr int SBW2_SA = 128 * 128, SBW2_SB = 96 * 128;  // dy slots of half A / B
+
+__global__ void __launch_bounds__(768, 1) conv_stem_bwd_wgrad2_kernel(const StemBwArgs a) {
+  typedef __bf16 T;
+  typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
+  constexpr int NB = 14;
+  constexpr int NVW = 8;  // dy waves (2 per SIMD); waves 8-11 run the MFMAs
+  static_assert(STEM_XBUF / 1024 >= NVW && (SBW_Y + SBW_DP + SBW_IX) / 1024 >= NVW, "padding re-issues block i - NVW");
+  static_assert(2 * SBW_IN + SBW2_SA + SBW2_SB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SBW_IN + SBW2_SA + SBW2_SB];
+  char* const SA = smem + 2 * SBW_IN;
+  char* const SB = SA + SBW2_SA;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool vw = wave < NVW;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int u0 = (int)((long)g * a.tiles / G), u1 = (int)((long)(g + 1) * a.tiles / G);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsY = make_rsrc(a.Y, a.y_bytes);
+  const __amdgpu_buffer_rsrc_t rsP = make_rsrc(a.DP, a.dp_bytes), rsI = make_rsrc(a.IX, a.ix_bytes);
+  const int xpitch = a.W * 8;
+  const int xrun = STEM_XROWS * xpitch;
+  const int yrun = 2 * a.Q * 128, prow = a.Q2 * 128, irow = a.Q2 * 64;
+  auto buf = [&](int tile) { return smem + ((tile - u0) & 1) * SBW_IN; };
+
+  // x rows of a tile (ceil(STEM_XBUF / NVW KiB) instructions per dy wave; a
+  // tile past the range issues zero-fill so every wave's count is fixed)
+  auto issue_x = [&](int tile) {
+    char* B = buf(tile);
+    const bool ok = tile < u1;
+    const int R0 = tile * 2;
+    const int n = R0 / a.P, h0 = R0 - n * a.P;
+    const uint32_t xb = (uint32_t)((((long)n * a.H + 2 * h0) * a.W) * 8);
+#pragma unroll
+    for (int k = 0; k < (STEM_XBUF / 1024 + NVW - 1) / NVW; ++k) {
+      // past the region: the wave's previous block again (same bytes to the same place)
+      const int i = wave + NVW * k - (wave + NVW * k < STEM_XBUF / 1024 ? 0 : NVW);
+      const int b = i * 1024 + lane * 16;
+      blds16(rsX, ok && b < xrun ? xb + (uint32_t)b : SSIP_OOB, B + i * 1024);
+    }
+  };
+  // y (whole 1-KiB runs), pooled gradient rows and argmax rows of a tile
+  auto issue_ypi = [&](int tile) {
+    char* B = buf(tile);
+    const bool ok = tile < u1;
+    const int R0 = tile * 2;
+    const int n = R0 / a.P, h0 = R0 - n * a.P, T0 = h0 >> 1;
+    const uint32_t yb = (uint32_t)((((long)n * a.P + h0) * a.Q) * 128);
+    const int prows = (T0 + 1 < a.P2) ? 2 : 1;
+    const uint32_t pb = (uint32_t)((((long)n * a.P2 + T0) * a.Q2) * 128);
+    const uint32_t ib = (uint32_t)((((long)n * a.P2 + T0) * a.Q2) * 64);
+    constexpr int NY = SBW_Y / 1024, NP = SBW_DP / 1024, NI = SBW_IX / 1024;
+#pragma unroll
+    for (int k = 0; k < (NY + NP + NI + NVW - 1) / NVW; ++k) {
+      // past the regions: the wave's previous block again (same bytes to the same place)
+      const int i = wave + NVW * k - (wave + NVW * k < NY + NP + NI ? 0 : NVW);
+      const int b = (i < NY ? i : (i < NY + NP ? i - NY : i - NY - NP)) * 1024 + lane * 16;
+      if (i < NY) {
+        blds16(rsY, ok && b < yrun ? yb + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + i * 1024);
+      } else if (i < NY + NP) {
+        blds16(rsP, ok && b < prows * prow ? pb + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + i * 1024);
+      } else {
+        blds16(rsI, ok && b < prows * irow ? ib + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + i * 1024);
+      }
+    }
+  };
+  constexpr int CX = (STEM_XBUF / 1024 + NVW - 1) / NVW;
+  constexpr int CY = ((SBW_Y + SBW_DP + SBW_IX) / 1024 + NVW - 1) / NVW;
+
+  // ---- dy waves: thread = (block lb, 4-channel quad c4) of a half
+  const int lb = tid >> 4, c4 = tid & 15, ch0 = c4 * 4;
+  float sc[4], sh[4], ca[4], cb[4], ck[4];
+  if (vw) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sc[e] = a.scale[ch0 + e];
+      sh[e] = a.shift[ch0 + e];
+      ca[e] = a.coef[ch0 + e];
+      cb[e] = a.coef[64 + ch0 + e];
+      ck[e] = a.coef[128 + ch0 + e];
+    }
+  }
+  // half h of tile `tile` into slot D (GEMM row of pixel (j, q) = chunk * 32 + j * 16 + q % 16,
+  // chunk = (q - q0) / 16 with q0 the half's first column)
+  auto produce = [&](int tile, int h, char* D) {
+    if (a.diag & 1) return;
+    const int nblk = h == 0 ? 32 : 24;
+    if (lb >= nblk) return;
+    const int R0 = tile * 2;
+    const int h0 = R0 - (R0 / a.P) * a.P, T0 = h0 >> 1;
+    const char* B = buf(tile);
+    const char* Ys = B + STEM_XBUF;
+    const char* Ps = Ys + SBW_Y;
+    const char* Is = Ps + SBW_DP;
+    const int l = (h == 0 ? 0 : 32) + lb;  // pooled window column: output columns 2l, 2l+1
+    const bool q1 = l + 1 < a.Q2, p1 = T0 + 1 < a.P2;
+    const uint32_t NOHIT = ~0u;  // no argmax byte is 255
+    uint32_t k00, k01 = NOHIT, k10 = NOHIT, k11 = NOHIT;
+    v4bf g00, g01, g10, g11;
+    const v4bf z4 = (v4bf){(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+    k00 = *reinterpret_cast<const uint32_t*>(Is + l * 64 + ch0);
+    g00 = *reinterpret_cast<const v4bf*>(Ps + l * 128 + ch0 * 2);
+    g01 = g10 = g11 = z4;
+    if (q1) {
+      k01 = *reinterpret_cast<const uint32_t*>(Is + (l + 1) * 64 + ch0);
+      g01 = *reinterpret_cast<const v4bf*>(Ps + (l + 1) * 128 + ch0 * 2);
+    }
+    if (p1) {
+      k10 = *reinterpret_cast<const uint32_t*>(Is + (a.Q2 + l) * 64 + ch0);
+      g10 = *reinterpret_cast<const v4bf*>(Ps + (a.Q2 + l) * 128 + ch0 * 2);
+      if (q1) {
+        k11 = *reinterpret_cast<const uint32_t*>(Is + (a.Q2 + l + 1) * 64 + ch0);
+        g11 = *reinterpret_cast<const v4bf*>(Ps + (a.Q2 + l + 1) * 128 + ch0 * 2);
+      }
+    }
+    float dz[4][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int b00 = (int)((k00 >> (8 * e)) & 0xff), b01 = (int)((k01 >> (8 * e)) & 0xff);
+      const int b10 = (int)((k10 >> (8 * e)) & 0xff), b11 = (int)((k11 >> (8 * e)) & 0xff);
+      const float v00 = (float)g00[e], v01 = (float)g01[e], v10 = (float)g10[e], v11 = (float)g11[e];
+      float d;
+      d = 0.f; if (b00 == 4) d += v00;
+      dz[0][e] = d;
+      d = 0.f; if (b00 == 5) d += v00; if (b01 == 3) d += v01;
+      dz[1][e] = d;
+      d = 0.f; if (b00 == 7) d += v00; if (b10 == 1) d += v10;
+      dz[2][e] = d;
+      d = 0.f; if (b00 == 8) d += v00; if (b01 == 6) d += v01; if (b10 == 2) d += v10; if (b11 == 0) d += v11;
+      dz[3][e] = d;
+    }
+    const int q0 = h == 0 ? 0 : 64;
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int q = 2 * l + (px & 1), j = px >> 1;
+      const int m = j * a.Q + q;                                      // pixel within the tile
+      const int r = ((q - q0) >> 4) * 32 + j * 16 + ((q - q0) & 15);  // GEMM row within the half
+      const v4bf yy = *reinterpret_cast<const v4bf*>(Ys + m * 128 + ch0 * 2);
+      v4bf o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float yv = (float)yy[e];
+        const float t = __builtin_fmaf(yv, sc[e], sh[e]);
+        const float d = (t > 0.f ? t : 0.f) > 0.f ? dz[px][e] : 0.f;
+        o[e] = (__bf16)(ca[e] * d + cb[e] * yv + ck[e]);
+      }
+      *reinterpret_cast<v4bf*>(D + r * 128 + (((c4 >> 1) ^ ((r & 3) << 1)) << 4) + (c4 & 1) * 8) = o;
+    }
+  };
+
+  // ---- MFMA waves: wave mw = wave - NVW owns column blocks mw + 4 b (b < nbw) x all 64 k
+  const int mw = wave - NVW;
+  const int nbw = mw < NB - 12 ? 4 : 3;
+  const int lg = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
+  auto consume = [&](f32x4 (&acc)[4][4], int tile, int h, const char* D) {
+    if (a.diag & 2) return;
+    const char* Xs = buf(tile);
+    const int nks = h == 0 ? 4 : 3, q0 = h == 0 ? 0 : 64;
+    for (int ks = 0; ks < nks; ++ks) {
+      Frag<T> fa[4], fb[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) read_tfrag(fa[x], D, 32 * ks, x * 16, lane);
+      // the lane's rows (lo, hi = lo + 4) of this chunk: output row >> 4, column q0 + 16 ks + (row & 15)
+      const int m_lo = 8 * lg + lq, m_hi = m_lo + 4;
+      const int base_lo = 2 * (m_lo >> 4) * xpitch + (q0 + 16 * ks + (m_lo & 15)) * 16;
+      const int base_hi = 2 * (m_hi >> 4) * xpitch + (q0 + 16 * ks + (m_hi & 15)) * 16;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (b < nbw) {
+          const int nb = mw + 4 * b, r = nb >> 1, cofs = ((nb & 1) * 16 + 4 * lp) * 2;
+          v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (__attribute__((address_space(3))) v4bf*)(Xs + base_lo + r * xpitch + cofs));
+          v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (__attribute__((address_space(3))) v4bf*)(Xs + base_hi + r * xpitch + cofs));
+          fb[b].v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (b < nbw) mma(acc[x][b], fa[x], fb[b]);
+    }
+  };
+
+  // the two roles run separate loops (so neither holds the other's registers)
+  // with the same barrier sequence: 2 in the prologue, 2 per tile
+  if (vw) {
+    if (u0 < u1) {
+      // prologue: inputs of the first tile (+ y / pooled / argmax of the second), its half A
+      issue_ypi(u0);
+      issue_x(u0);
+      issue_ypi(u0 + 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CY) : "memory");
+      halo_lds_barrier();
+      produce(u0, 0, SA);
+      halo_lds_barrier();
+    }
+    for (int u = u0; u < u1; ++u) {
+      // phase (u, A): dy (u, B) beside the MFMAs of (u, A); x of u+1 into its buffer
+      issue_x(u + 1);
+      produce(u, 1, SB);
+      // y / pooled / argmax of u+1 (issued at (u-1, B)) land before the barrier
+      // ahead of phase (u, B), whose dy waves form (u+1, A); younger: x of u+1
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CX) : "memory");
+      halo_lds_barrier();
+      // phase (u, B): dy (u+1, A) beside the MFMAs of (u, B); y / pooled / argmax of u+2
+      issue_ypi(u + 2);
+      if (u + 1 < u1) produce(u + 1, 0, SA);
+      // x of u+1 (issued at (u, A)) lands before the barrier ahead of (u+1, A);
+      // younger: this phase's y / pooled / argmax of u+2
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CY) : "memory");
+      halo_lds_barrier();
+    }
+    // the zero-fill issues past the range land before the LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[x][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (u0 < u1) {
+      halo_lds_barrier();
+      halo_lds_barrier();
+    }
+    for (int u = u0; u < u1; ++u) {
+      consume(acc, u, 0, SA);
+      halo_lds_barrier();
+      consume(acc, u, 1, SB);
+      halo_lds_barrier();
+    }
+    float* sl = a.slab + (long)g * 64 * 224;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (b < nbw)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int kk = x * 16 + 4 * (lane >> 4) + e;
+            const int col = (mw + 4 * b) * 16 + (lane & 15);
+            sl[(long)kk * 224 + col] = acc[x][b][e];
+          }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host-side planning
 // ---------------------------------------------------------------------------
@@ -4322,7 +4588,12 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
     if (diag & 4) h.x_bytes = h.y_bytes = h.dp_bytes = h.ix_bytes = 0;  // zero-extent: no memory traffic
   }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv_stem_bwd_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+  // SSIP_STEM_BW=1: the kernel with every wave in both halves (A/B)
+  static const int v1 = getenv("SSIP_STEM_BW") ? atoi(getenv("SSIP_STEM_BW")) : 0;
+  if (v1 == 1)
+    hipLaunchKernelGGL(conv_stem_bwd_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+  else
+    hipLaunchKernelGGL(conv_stem_bwd_wgrad2_kernel, dim3(hp.G), dim3(768), 0, st, h);
   int rc = ::ssip::check_launch("conv_stem_bwd_wgrad");
   if (rc) return rc;
   const long total4 = 64L * 224 / 4;

@@ -265,11 +265,22 @@ class SemiStep:
         holds every SIMD's register file, so the first update is dispatched
         as it drains rather than beside it: profiles/r2_step_streams.txt.)"""
         m = self.model
+        late = {id(m.conv1.weight)}
+        oside = m.take_opt_side()
+        if oside is not None:
+            # the stem wgrad is on main: every other update on the side stream
+            # beside it (this launch advances the device schedule), conv1's
+            # after both, on main
+            main = torch.cuda.current_stream()
+            with torch.cuda.stream(oside):
+                self.opt.step(grad_scale=scale, skip=late, join_pending=False)
+            ops.wait_stream(main, oside)
+            self.opt.step(grad_scale=scale, only=late, sched_step=False)
+            return
         pend = m.take_pending_side()
         if pend is None:
             self.opt.step(grad_scale=scale)
             return
-        late = {id(m.conv1.weight)}
         self.opt.step(grad_scale=scale, skip=late, join_pending=False)
         ops.wait_stream(torch.cuda.current_stream(), pend)
         self.opt.step(grad_scale=scale, only=late, sched_step=False)

@@ -50,13 +50,13 @@ __device__ __forceinline__ void bn_fin_write(int c, const BnFwdFin& f, double N,
 // mean K (the shifted-data form of the pairwise merge):
 //   n = sum n_t,  s = sum n_t (mean_t - K),  q = sum M2_t + n_t (mean_t - K)^2
 //   mean = K + s / n,  M2 = q - s^2 / n.
-// Threads take FIN_PT records at a time, FIN_NT apart, in increasing order;
-// wave butterflies and a 4-entry LDS combine in fixed order keep the result
-// reproducible.  S == 1 writes the statistics; otherwise {n, mean, M2} of the
-// split go to scratch[c][s] for bn_finalize_merge_kernel.
-__global__ void __launch_bounds__(FIN_NT) bn_finalize_kernel(int C, int tiles, int S, const float* __restrict__ partial,
-                                                             double* scratch, BnFwdFin f) {
-  __shared__ double sh[3 * 4];
+// Threads take FIN_PT records at a time, NT apart, in increasing order; wave
+// butterflies and (NT = 256) a 4-entry LDS combine in fixed order keep the
+// result reproducible.  S == 1 writes the statistics; otherwise {n, mean, M2}
+// of the split go to scratch[c][s] for bn_finalize_merge_kernel.
+template <int NT>
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(int C, int tiles, int S, const float* __restrict__ partial,
+                                                        double* scratch, BnFwdFin f) {
   const int c = blockIdx.y, s = blockIdx.x;
   const float* rec = partial + (long)c * tiles * 3;
   const int L = (tiles + S - 1) / S;
@@ -67,11 +67,11 @@ __global__ void __launch_bounds__(FIN_NT) bn_finalize_kernel(int C, int tiles, i
     K = n0 > 0.0 ? (double)rec[(long)t0 * 3 + 1] / n0 : 0.0;
   }
   double v[3] = {0.0, 0.0, 0.0};
-  for (int base = t0 + threadIdx.x; base < t1; base += FIN_NT * FIN_PT) {
+  for (int base = t0 + threadIdx.x; base < t1; base += NT * FIN_PT) {
     float r[FIN_PT][3];
 #pragma unroll
     for (int i = 0; i < FIN_PT; ++i) {
-      const int t = base + i * FIN_NT;
+      const int t = base + i * NT;
       const bool ok = t < t1;
       r[i][0] = ok ? rec[(long)t * 3] : 0.f;
       r[i][1] = ok ? rec[(long)t * 3 + 1] : 0.f;
@@ -88,7 +88,12 @@ __global__ void __launch_bounds__(FIN_NT) bn_finalize_kernel(int C, int tiles, i
       }
     }
   }
-  block_sums_f64_256<3>(v, sh);
+  if constexpr (NT == 64) {
+    wave_sums_f64<3>(v);
+  } else {
+    __shared__ double sh[3 * 4];
+    block_sums_f64_256<3>(v, sh);
+  }
   if (threadIdx.x == 0) {
     const double N = v[0];
     const double mu = N > 0.0 ? K + v[1] / N : 0.0;
@@ -253,6 +258,65 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, co
     g0.load(dz + (long)i * 8);
     y0.load(y + (long)i * 8);
     if (zmask) z0.load(zmask + (long)i * 8);
+    one(g0, z0, y0, i);
+  }
+}
+
+// bn_bwd_apply_kernel with 4 channels per thread, bf16 only, held to 64
+// VGPRs (the 8-channel form takes 104) so it runs beside a resident wgrad
+// (see bn_bwd_reduce4_kernel).  Same per-element formula.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
+bn_bwd_apply4_kernel(int total4, int C, const __bf16* __restrict__ dz, const __bf16* __restrict__ zmask,
+                     const uint8_t* __restrict__ mbits, const __bf16* __restrict__ y,
+                     const float* __restrict__ coef, __bf16* __restrict__ dy, __bf16* __restrict__ dpre,
+                     const float* __restrict__ mscale, const float* __restrict__ mshift) {
+  const int cpr = C >> 2;
+  const int start = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (start % cpr) * 4;
+  const bool amask = mscale != nullptr;
+  const float4 ca = *reinterpret_cast<const float4*>(coef + c0);
+  const float4 cb = *reinterpret_cast<const float4*>(coef + C + c0);
+  const float4 cc = *reinterpret_cast<const float4*>(coef + 2 * C + c0);
+  float4 msc = make_float4(0.f, 0.f, 0.f, 0.f), msh = msc;
+  if (amask) {
+    msc = *reinterpret_cast<const float4*>(mscale + c0);
+    msh = *reinterpret_cast<const float4*>(mshift + c0);
+  }
+  const bf16x4 zero4 = (bf16x4){(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+  const int stride = gridDim.x * blockDim.x;
+  auto one = [&](bf16x4 g, bf16x4 zz, bf16x4 yy, int i) {
+    const float a_[4] = {ca.x, ca.y, ca.z, ca.w}, b_[4] = {cb.x, cb.y, cb.z, cb.w}, c_[4] = {cc.x, cc.y, cc.z, cc.w};
+    const float s_[4] = {msc.x, msc.y, msc.z, msc.w}, h_[4] = {msh.x, msh.y, msh.z, msh.w};
+    const uint32_t mb = mbits ? ((uint32_t)mbits[i >> 1] >> ((i & 1) * 4)) : 0xFu;
+    bf16x4 o, p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = (float)g[j];
+      const float yv = (float)yy[j];
+      if (zmask) d = (float)zz[j] > 0.f ? d : 0.f;
+      if (amask) d = __builtin_fmaf(yv, s_[j], h_[j]) > 0.f ? d : 0.f;
+      d = ((mb >> j) & 1u) ? d : 0.f;
+      p[j] = (__bf16)d;
+      o[j] = (__bf16)(a_[j] * d + b_[j] * yv + c_[j]);
+    }
+    *reinterpret_cast<bf16x4*>(dy + (long)i * 4) = o;
+    if (dpre) *reinterpret_cast<bf16x4*>(dpre + (long)i * 4) = p;
+  };
+  int i = start;
+  for (; i + stride < total4; i += 2 * stride) {
+    const bf16x4 g0 = *reinterpret_cast<const bf16x4*>(dz + (long)i * 4);
+    const bf16x4 g1 = *reinterpret_cast<const bf16x4*>(dz + (long)(i + stride) * 4);
+    const bf16x4 y0 = *reinterpret_cast<const bf16x4*>(y + (long)i * 4);
+    const bf16x4 y1 = *reinterpret_cast<const bf16x4*>(y + (long)(i + stride) * 4);
+    const bf16x4 z0 = zmask ? *reinterpret_cast<const bf16x4*>(zmask + (long)i * 4) : zero4;
+    const bf16x4 z1 = zmask ? *reinterpret_cast<const bf16x4*>(zmask + (long)(i + stride) * 4) : zero4;
+    one(g0, z0, y0, i);
+    one(g1, z1, y1, i + stride);
+  }
+  if (i < total4) {
+    const bf16x4 g0 = *reinterpret_cast<const bf16x4*>(dz + (long)i * 4);
+    const bf16x4 y0 = *reinterpret_cast<const bf16x4*>(y + (long)i * 4);
+    const bf16x4 z0 = zmask ? *reinterpret_cast<const bf16x4*>(zmask + (long)i * 4) : zero4;
     one(g0, z0, y0, i);
   }
 }
@@ -436,8 +500,12 @@ int ssip_bn_finalize(int C, int tiles, float* partial, const float* gamma, const
                    mean_out, invstd_out, scale_out, shift_out};
   const int S = fin_splits(tiles);
   double* scratch = fin_scratch(partial, (int64_t)C * tiles * 3);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S, (const float*)partial, scratch,
-                     f);
+  if (fin_nt() == 64)
+    hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3(S, C), dim3(64), 0, st, C, tiles, S, (const float*)partial,
+                       scratch, f);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(S, C), dim3(256), 0, st, C, tiles, S, (const float*)partial,
+                       scratch, f);
   if (S > 1)
     hipLaunchKernelGGL(bn_finalize_merge_kernel, dim3((C + FIN_NT / 64 - 1) / (FIN_NT / 64)), dim3(FIN_NT), 0, st,
                        C, S, (const double*)scratch, f);
@@ -546,15 +614,29 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   const int blocks = (int)((M + rows - 1) / rows);
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_bwd: unsupported size");
   const int total8 = (int)(M * C / 8);
+  // SSIP_BWD_REDUCE4=1 / SSIP_BWD_APPLY4=1: the 64-VGPR 4-channel forms (opt-in:
+  // running beside the wgrads they made the step slower, 6.70 vs 6.50 ms)
+  static const bool red4 = getenv("SSIP_BWD_REDUCE4") && atoi(getenv("SSIP_BWD_REDUCE4")) != 0;
+  static const bool apply4 = getenv("SSIP_BWD_APPLY4") && atoi(getenv("SSIP_BWD_APPLY4")) != 0;
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
-                       (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
+    if (sizeof(T) == 2 && red4 && C / 4 <= 256 && 256 % (C / 4) == 0)
+      hipLaunchKernelGGL(bn_bwd_reduce4_kernel, dim3(blocks), dim3(256), 0, st, (long)M, C, rows,
+                         (const __bf16*)dz, (const __bf16*)zmask, mbits, (const __bf16*)y, mean, invstd, mscale,
+                         mshift, partial);
+    else
+      hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
+                         (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
     BnBwdFin f;
     f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
                               fin_scratch(partial, (int64_t)blocks * C * 2));
     launch_bn_bwd_finalize(st, C, blocks, (long)M, 1, 1, f, accumulate);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dz,
-                       (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
+    if (sizeof(T) == 2 && apply4 && C / 4 <= 256 && 256 % (C / 4) == 0 && M * C / 4 < (1l << 31))
+      hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(bn_elem_grid(2 * (long)total8)), dim3(256), 0, st,
+                         (int)(2 * (long)total8), C, (const __bf16*)dz, (const __bf16*)zmask, mbits,
+                         (const __bf16*)y, coef, (__bf16*)dy, (__bf16*)dpre, mscale, mshift);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
+                         (const T*)dz, (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
 }

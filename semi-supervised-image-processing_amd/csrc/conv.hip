@@ -3700,10 +3700,14 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
                "the 8-phase kernel has no stride-2 dgrad phase split");
   SSIP_REQUIRE(pl.stages != 8 || MODE != MODE_WGRAD || (pl.args.C % 256 == 0 && pl.args.K % 256 == 0), SSIP_ERR_ARG,
                "the 8-phase wgrad needs C and K multiples of 256 (one tap per 256-column tile)");
+  // SSIP_WG_LDSPAD (tuning): extra LDS bytes per wgrad workgroup, to cap how
+  // many share a CU with the main stream's kernels
+  static const int wg_ldspad = getenv("SSIP_WG_LDSPAD") ? atoi(getenv("SSIP_WG_LDSPAD")) : 0;
+  const unsigned dyn_lds = MODE == MODE_WGRAD ? (unsigned)wg_ldspad : 0u;
 #define SSIP_GLDS_GO(BM_, BN_, WM_, WN_, ST_)                                                                 \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
-                       st, pl.args);                                                                          \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_),      \
+                       dyn_lds, st, pl.args);                                                                 \
     return ::ssip::check_launch("conv_glds");                                                                 \
   }
   {

@@ -1,7 +1,7 @@
 """BatchNorm finalize (forward statistics and backward coefficients) over
-record counts either side of the split point (ABI 9: more than 2048 records
-per channel are merged by several 256-thread workgroups plus a one-wave merge
-pass).  Reference: the same records merged on the host in float64 (Chan's
+record counts either side of the split point (more than 2048 records per
+channel are merged by several 256-thread workgroups plus a one-wave merge
+pass; 512 with SSIP_FIN_NT=64's one-wave workgroups).  Reference: the same records merged on the host in float64 (Chan's
 pairwise formula for {count, sum, M2}; plain sums for the backward), i.e. the
 batch mean / biased variance torchvision's BatchNorm2d uses
 (src/training/common.py:380 `model(inputs)` in train mode).  Tolerance:
@@ -38,7 +38,7 @@ def _host_stats(rec):
     return N, mean, M2 / N
 
 
-@pytest.mark.parametrize("C,tiles,empty", [(64, 1, 0), (64, 2048, 0), (64, 2049, 0), (128, 5000, 7),
+@pytest.mark.parametrize("C,tiles,empty", [(64, 1, 0), (64, 513, 0), (64, 2048, 0), (64, 2049, 0), (128, 5000, 7),
                                            (64, 18816, 0), (8, 140000, 0)])
 def test_bn_finalize_split(dev, C, tiles, empty):
     rec = _records(C, tiles, seed=tiles + C, empty_every=empty)
@@ -75,7 +75,7 @@ def test_bn_finalize_split(dev, C, tiles, empty):
     assert torch.equal(st, st2)
 
 
-@pytest.mark.parametrize("tiles", [512, 2049, 9408])
+@pytest.mark.parametrize("tiles", [512, 513, 2049, 9408])
 def test_bn_bwd_from_partials_split(dev, tiles):
     """[C][tiles][2] sums of dout and dout*xhat (the dgrad-fused BN reduction)
     -> dgamma / dbeta and dy = dBN(dout), split finalize included."""

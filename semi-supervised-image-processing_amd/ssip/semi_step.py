@@ -33,6 +33,11 @@ from .optim import AdamW
 from .resnet import DeviceImages, SSIPResNet
 
 
+# the weight refresh on the side stream beside the train views' augment
+# (SSIP_PREP_SIDE=0: on main ahead of both)
+_PREP_SIDE = os.environ.get("SSIP_PREP_SIDE", "1") != "0"
+
+
 @dataclass
 class StepStats:
     # [4] total, L_l, L_u, mask count (device).  In plan mode every replay
@@ -174,18 +179,25 @@ class SemiStep:
         m.bn_update_running = True
         return zw
 
-    def _train_fwd(self, x_l, x_u, pl, ps) -> torch.Tensor:
-        """[labelled weak ; unlabelled strong] views and the joint train forward."""
+    def _train_views(self, x_l, x_u, pl, ps) -> torch.Tensor:
+        """[labelled weak ; unlabelled strong] views of the joint train forward."""
         m = self.model
         Bl, Bu = x_l.shape[0], x_u.shape[0]
         S, P = self.size, self.tf.pad
         x_ls = torch.empty((Bl + Bu, S + 2 * P, S + 2 * P, 4), device=x_l.device, dtype=m.compute_dtype)
         self.tf(x_l, pl, out=x_ls[:Bl])
         self.tf(x_u, ps, out=x_ls[Bl:])
+        return x_ls
+
+    def _train_fwd(self, x_l, x_u, pl, ps, x_ls=None) -> torch.Tensor:
+        """The joint train forward (views formed here unless given)."""
+        m = self.model
+        if x_ls is None:
+            x_ls = self._train_views(x_l, x_u, pl, ps)
         self.opt.zero_grad(set_to_none=True)
         if self.bucketer is not None:
             self.bucketer.reset()
-        return m(DeviceImages(x_ls, P))
+        return m(DeviceImages(x_ls, self.tf.pad))
 
     def _loss_bwd(self, logits, y_l, zw) -> torch.Tensor:
         """loss + dlogits in one launch, then the backward."""
@@ -204,14 +216,27 @@ class SemiStep:
         dev = x_l.device
         main = torch.cuda.current_stream(dev)
         m.train()
-        # compute-dtype weights for both forwards, refreshed once, before the fork
-        m.prepare_weights(need_t=True)
         side = self._side_stream(dev) if self.overlap else main
-        if side is not main:
+        if side is not main and _PREP_SIDE:
+            # the compute-dtype weight refresh for both forwards on the side
+            # stream, beside the train views' augment on main; main waits for
+            # the refresh (not for the weak forward queued after it)
             ops.wait_stream(side, main)
-        with torch.cuda.stream(side):
-            zw = self._weak(x_u, pw)
-        logits = self._train_fwd(x_l, x_u, pl, ps)
+            with torch.cuda.stream(side):
+                m.prepare_weights(need_t=True)
+            x_ls = self._train_views(x_l, x_u, pl, ps)
+            ops.wait_stream(main, side)
+            with torch.cuda.stream(side):
+                zw = self._weak(x_u, pw)
+            logits = self._train_fwd(x_l, x_u, pl, ps, x_ls)
+        else:
+            # compute-dtype weights for both forwards, refreshed once, before the fork
+            m.prepare_weights(need_t=True)
+            if side is not main:
+                ops.wait_stream(side, main)
+            with torch.cuda.stream(side):
+                zw = self._weak(x_u, pw)
+            logits = self._train_fwd(x_l, x_u, pl, ps)
         if side is not main:
             ops.wait_stream(main, side)
             zw.record_stream(main)

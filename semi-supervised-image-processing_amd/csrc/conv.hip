@@ -3213,8 +3213,9 @@ __global__ void __launch_bounds__(512, 2) conv_stem_bwd_wgrad_kernel(const StemB
 // The same fused stem backward tail with the two halves specialised
 // (tools/time_stem_bw.py: DMA + sync alone 133 us, the dy pass +72, the
 // MFMAs +74, and the two do not overlap in conv_stem_bwd_wgrad_kernel, where
-// every wave runs both behind a barrier): waves 0-3 form dy, waves 4-7
-// multiply.  A tile's 224 GEMM rows are cut into half A (output columns
+// every wave runs both behind a barrier): waves 0-7 form dy (two per SIMD,
+// 4 channels x one 2x2 block per thread), waves 8-11 multiply (one per SIMD,
+// all 64 k x 3-4 column blocks).  A tile's 224 GEMM rows are cut into half A (output columns
 // 0-63 of both rows: 128 rows, 4 k-steps) and half B (columns 64-111: 96
 // rows, 3 k-steps), GEMM row = 16 columns x 2 rows per 32-row chunk (the
 // 2x2 pixel blocks of 8 pooled windows).  Phase (u, A): the dy waves form

@@ -76,9 +76,15 @@ __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __r
     m[i] = mi;
     v[i] = vi;
   }
-  if (advance && threadIdx.x == 0) {
+  if (advance) {
+    // every wave of this workgroup has read the schedule (its loads retired at
+    // the barrier) before the workgroup counts as arrived; the release half
+    // of the acq_rel add orders those reads before the arrival, the acquire
+    // half orders the last arriver's stores after every other arrival
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(sched + 4);
-    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (old == gridDim.x - 1) {
       sched[1] = t;
       sched[2] = ss;

@@ -62,7 +62,9 @@ def shard_loader(loader: DataLoader, even: bool = False) -> DataLoader:
     """This rank's contiguous run of the loader's batches (same batch size,
     collate and workers; sequential loaders only).  even=True (training: every
     batch is a step with gradient all-reduces, so every rank must run the same
-    number) keeps only the first world * floor(nb / world) batches."""
+    number) pads the batch list to a multiple of world by wrapping around to
+    its first batches, as RankStridedSampler / DistributedSampler pad: every
+    rank runs ceil(nb / world) batches and no batch of the epoch is dropped."""
     w = world()
     if w == 1:
         return loader
@@ -71,12 +73,16 @@ def shard_loader(loader: DataLoader, even: bool = False) -> DataLoader:
     ds = loader.dataset
     n, bs = len(ds), loader.batch_size
     nb = math.ceil(n / bs) if not loader.drop_last else n // bs
-    if even:
-        nb -= nb % w
-    blo, bhi = shard_range(nb, rank(), w)
-    idx = list(range(blo * bs, min(bhi * bs, n)))
-    return DataLoader(Subset(ds, idx), batch_size=bs, shuffle=False, num_workers=loader.num_workers,
-                      pin_memory=loader.pin_memory, collate_fn=loader.collate_fn, drop_last=loader.drop_last)
+    if not even:
+        blo, bhi = shard_range(nb, rank(), w)
+        idx = list(range(blo * bs, min(bhi * bs, n)))
+        return DataLoader(Subset(ds, idx), batch_size=bs, shuffle=False, num_workers=loader.num_workers,
+                          pin_memory=loader.pin_memory, collate_fn=loader.collate_fn, drop_last=loader.drop_last)
+    total = -(-nb // w) * w if nb > 0 else 0
+    blo, bhi = shard_range(total, rank(), w)
+    batches = [list(range((b % nb) * bs, min((b % nb + 1) * bs, n))) for b in range(blo, bhi)]
+    return DataLoader(ds, batch_sampler=batches, num_workers=loader.num_workers, pin_memory=loader.pin_memory,
+                      collate_fn=loader.collate_fn)
 
 
 def gather_list(local: list) -> list:

@@ -151,16 +151,19 @@ class SemiStep:
         self._pin_ring[i] = (buf, None)
         return buf
 
-    def _pinned_read(self, t) -> None:
-        """Mark the ring slot holding host tensor t as read by the stream's latest copy."""
-        if t is None:
-            return
+    def _pinned_read(self, *ts) -> None:
+        """Mark every ring slot that holds (part of) a host tensor in ts as read
+        by the current stream's latest copy: the slot is handed out again only
+        after that copy has run.  Called after every non_blocking copy out of
+        the ring (eager, plan and graph paths alike)."""
         for i, (buf, _) in enumerate(self._pin_ring):
-            if buf is not None and buf.data_ptr() == t.data_ptr():
+            if buf is None:
+                continue
+            lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * buf.element_size()
+            if any(t is not None and t.device.type == "cpu" and lo <= t.data_ptr() < hi for t in ts):
                 ev = torch.cuda.Event()
                 ev.record()
                 self._pin_ring[i] = (buf, ev)
-                return
 
     def input_slots(self):
         """The device buffers a recorded plan reads its batch from
@@ -262,7 +265,7 @@ class SemiStep:
     def _eager_step(self, x_l, y_l, x_u, params) -> StepStats:
         dev = x_l.device
         pl, pw, ps = (p.to(dev, non_blocking=True) for p in params)
-        self._pinned_read(_common_base(params))
+        self._pinned_read(*params)
         out = self._fwd_bwd(x_l, y_l, x_u, pl, pw, ps)
         scale = self.bucketer.finish() if self.bucketer is not None else 1.0
         # 6. optimizer
@@ -348,10 +351,10 @@ class SemiStep:
         base = _common_base(params)
         if base is not None and self._static_pbase is not None and base.shape == self._static_pbase.shape:
             self._static_pbase.copy_(base, non_blocking=True)
-            self._pinned_read(base)
         else:
             for dst, src in zip(self._static[3:], params):
                 dst.copy_(src, non_blocking=True)
+        self._pinned_read(*params)
         if self.bucketer is not None:
             self.bucketer.reset()
         if self.max_inflight > 0:
@@ -377,6 +380,7 @@ class SemiStep:
             for dst, src in zip(self._static, (x_l, y_l, x_u) + tuple(params)):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src, non_blocking=True)
+            self._pinned_read(*params)
         self._g.replay()
         if self.bucketer is not None:
             self.bucketer.launch_after_graph()

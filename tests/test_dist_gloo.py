@@ -137,8 +137,15 @@ def _pipeline_worker(rank, world, port, q):
             nbat = len(list(DataLoader(list(range(n)), batch_size=bs, sampler=smp)))
             ok &= len(set(D.gather_list([nbat]))) == 1
             even = D.shard_loader(DataLoader(list(range(n)), batch_size=bs, shuffle=False, drop_last=True), even=True)
-            counts = D.gather_list([len(list(even))])
-            ok &= len(set(counts)) == 1 and counts[0] == (n // bs) // world
+            got = [b.tolist() for b in even]
+            counts = D.gather_list([len(got)])
+            nb = n // bs
+            ok &= len(set(counts)) == 1 and counts[0] == -(-nb // world)
+            # no batch dropped: the rank-ordered batches are the single-process
+            # batches, wrapped around to the first ones up to a multiple of world
+            single_b = [list(range(b * bs, (b + 1) * bs)) for b in range(nb)]
+            allb = [b for part in D.gather_list([got]) for b in part]
+            ok &= allb == [single_b[i % nb] for i in range(len(allb))]
         # rank 0's BN buffers on every rank, bitwise
         bn = torch.nn.Sequential(torch.nn.BatchNorm2d(5), torch.nn.BatchNorm2d(3))
         bn.train()

@@ -261,6 +261,31 @@ def test_adamw_device_schedule_fused_advance(dev):
         assert _rel(ps[k].detach(), ref[k].detach()) < 1e-6, k
 
 
+@pytest.mark.parametrize("n", [5, 3 * 256 + 10])
+def test_adamw_dev_advance_small_n(dev, n):
+    """An advancing ssip_adamw_dev launch whose threads own at most one
+    element (n < 256 * workgroups: most waves of a workgroup have no element
+    and finish at once) advances t exactly once per launch, and every element
+    is updated with that launch's bias corrections (the arrival
+    count must wait for every wave's schedule read).  40 steps vs torch."""
+    torch.manual_seed(3)
+    p0 = torch.randn(n)
+    ref = torch.nn.Parameter(p0.clone())
+    topt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
+    p = p0.clone().to(dev)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    sched = torch.tensor([1e-3, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+    for _ in range(40):
+        g = torch.randn(n)
+        ref.grad = g.clone()
+        topt.step()
+        ops.adamw_dev(p, g.to(dev), m, v, sched, 0.9, 0.999, 1e-8, 1e-2, advance=True)
+    torch.cuda.synchronize()
+    s = sched.cpu()
+    assert s[1].item() == 40.0 and s[4].item() == 0.0
+    assert _rel(p, ref.detach()) < 1e-6
+
+
 @pytest.mark.parametrize("dtname", ["f32", "bf16"])
 def test_weight_prep_batch_layouts(dev, dtname):
     """Batched prep == the per-tensor layouts (exact): KRSC / CRSK, zero

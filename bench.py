@@ -68,10 +68,15 @@ def parse():
                     help="semi: the north-star train step (default); extract: src.feature_extraction's frozen "
                          "ResNet-18 embedding pass (the reference's only published throughput, 358.6 images/s)")
     ap.add_argument("--extract-images", type=int, default=1506, help="images of the end-to-end extraction run")
-    ap.add_argument("--cpu-warmup", type=int, default=1,
-                    help="CPU-baseline warm-up steps (BASELINE.md section 3 asks >= 10: pass --cpu-warmup 10 "
-                         "--cpu-steps 50 for the full protocol, ~6-7 min on 16 host cores)")
-    ap.add_argument("--cpu-steps", type=int, default=4, help="CPU-baseline timed steps (median reported)")
+    ap.add_argument("--cpu-warmup", type=int, default=10,
+                    help="CPU-baseline warm-up steps (BASELINE.md section 3: >= 10)")
+    ap.add_argument("--cpu-steps", type=int, default=50, help="CPU-baseline timed steps, median reported "
+                    "(BASELINE.md section 3: >= 50)")
+    ap.add_argument("--cpu-budget-s", type=float, default=340.0,
+                    help="stop the CPU-baseline timed steps after this much wall time (the count timed is reported)")
+    ap.add_argument("--cpu-batch", type=int, default=None,
+                    help="images per CPU-baseline step (default: the GPU batch; 16 for resnet50 at 512, where one "
+                         "full 128-image CPU step takes minutes)")
     ap.add_argument("--max-inflight", type=int, default=None,
                     help="host waits for step k - N before enqueueing step k (0: never; default: SemiStep's own "
                          "bound on launch-plan replays, $SSIP_MAX_INFLIGHT or 2)")
@@ -93,6 +98,56 @@ def host_cores() -> dict:
         pass
     cores = avail if quota is None else max(1, min(avail, int(quota + 0.5)))
     return {"cores": cores, "affinity": avail, "cgroup_quota": quota, "total": os.cpu_count()}
+
+
+class SclkSampler:
+    """Mean graphics clock (SCLK, MHz) of the bench's GPU over a timed region,
+    sampled every 5 ms from the SMU (amdsmi, by the device's PCI address).  A
+    box indicator only: the in-kernel clock under MFMA load can read up to
+    ~10 % below it (MI355X_MICROARCH.md, DVFS give-back)."""
+
+    def __init__(self, dev_index: int):
+        import threading
+
+        self.samples, self._stop, self.source, self.err = [], threading.Event(), None, None
+        try:
+            import amdsmi
+
+            p = torch.cuda.get_device_properties(dev_index)
+            bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+            amdsmi.amdsmi_init()
+            self._h = amdsmi.amdsmi_get_processor_handle_from_bdf(bdf)
+            self._read = lambda: float(amdsmi.amdsmi_get_clock_info(self._h, amdsmi.AmdSmiClkType.SYS)["clk"])
+            self._read()
+            self.source = f"amdsmi SYS clock of {bdf}"
+        except Exception as e:  # no SMU access on this box: report null
+            self._read, self.err = None, f"{type(e).__name__}: {e}"[:120]
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                self.samples.append(self._read())
+            except Exception:
+                pass
+            self._stop.wait(0.005)
+
+    def __enter__(self):
+        if self._read is not None:
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._read is not None:
+            self._t.join()
+
+    def summary(self):
+        if not self.samples:
+            return {"mean_mhz": None, "source": self.source, "error": self.err}
+        v = self.samples
+        return {"mean_mhz": round(sum(v) / len(v), 1), "min_mhz": min(v), "max_mhz": max(v), "samples": len(v),
+                "source": self.source}
 
 
 def extract_bench(args):
@@ -225,18 +280,40 @@ def main():
     torch.cuda.synchronize()
     if args.max_inflight is not None:
         step.max_inflight = args.max_inflight
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step(x_l, y_l, x_u)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with SclkSampler(local) as sclk:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step(x_l, y_l, x_u)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = out.loss.cpu().tolist()
+
+    # step boundaries (after the timed region, same replay path): events on the
+    # launch stream at each step's start and end; the stream's idle time
+    # between one step's last launch and the next step's first is the time the
+    # device waited for the host, and the host's own enqueue time per step
+    bounds, enq = [], []
+    for _ in range(8):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        h0 = time.perf_counter()
+        step(x_l, y_l, x_u)
+        enq.append(time.perf_counter() - h0)
+        e1.record()
+        bounds.append((e0, e1))
+    torch.cuda.synchronize()
+    gaps = sorted(bounds[i][1].elapsed_time(bounds[i + 1][0]) * 1e3 for i in range(len(bounds) - 1))
+    enq.sort()
+    boundary = {"gap_us_median": round(gaps[len(gaps) // 2], 1), "gap_us_max": round(gaps[-1], 1),
+                "host_enqueue_ms_median": round(enq[len(enq) // 2] * 1e3, 3),
+                "note": "launch-stream idle between consecutive steps (event after step k's last launch to "
+                        "event before step k+1's first), 8 untraced steps after the timed region"}
 
     # roofline leg: one instrumented step, HIP events around every conv launch.
     # Two more (unsynchronised) steps are queued first so the host enqueues
@@ -287,15 +364,21 @@ def main():
 
         # one thread per host core this process may use
         hc = host_cores()
-        c = time_cpu_step(Bl=Bl, Bu=Bu, steps=args.cpu_steps, warmup=args.cpu_warmup, threads=hc["cores"])
-        full = args.cpu_warmup >= 10 and args.cpu_steps >= 50
+        cb = args.cpu_batch or (16 if (args.arch, S) == ("resnet50", 512) else args.batch)
+        cbl = max(1, cb * Bl // args.batch)
+        c = time_cpu_step(Bl=cbl, Bu=cb - cbl, steps=args.cpu_steps, warmup=args.cpu_warmup, threads=hc["cores"],
+                          arch=args.arch, size=S, budget_s=args.cpu_budget_s)
+        full = c["warmup"] >= 10 and c["steps_timed"] >= 50
         cpu = {"value": round(c["value"], 3), "unit": "images/s", "cores": c["threads"], "kind": "port",
                "threads": c["threads"], "host_cores": hc["cores"], "host_cpus_affinity": hc["affinity"],
                "host_cgroup_quota": hc["cgroup_quota"], "host_cpus_total": hc["total"],
+               "model": args.arch, "image_size": S, "batch": cb,
                "sample": c["sample"] + ("" if full else
-                                        "; reduced from BASELINE.md section 3's >=10 warm-up + median of >=50 "
-                                        "timed steps to bound the bench's run time (full protocol: "
-                                        "--cpu-warmup 10 --cpu-steps 50)"),
+                                        f"; BASELINE.md section 3 asks >= 10 warm-up + >= 50 timed steps: "
+                                        f"{c['steps_timed']} fitted the --cpu-budget-s {args.cpu_budget_s:g} s "
+                                        "bound on the bench's run time")
+                         + ("" if cb == args.batch else f"; {cb} images per CPU step (the GPU step's "
+                                                        f"{args.batch} take minutes per CPU step), rate per image"),
                "step_times_s": [round(t, 3) for t in c["step_times_s"]]}
 
     if rank == 0:
@@ -333,6 +416,8 @@ def main():
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
                                    f"in {conv_ms:.3f} ms"},
             "cpu_baseline": cpu,
+            "sclk": sclk.summary(),
+            "step_boundary": boundary,
             "last_loss": [round(v, 5) for v in loss],
         }
         print(json.dumps(res))

@@ -6,7 +6,7 @@ ssip.semi_step.SemiStep, with the reference's own pieces:
             rotate -> ToTensor -> Normalize, src/training/common.py:96-119),
             strong view = the same ops with a +-30 deg rotation plus
             brightness/contrast jitter and a cutout square
-  model     torchvision resnet18 (restated in oracle/torchvision_restate)
+  model     torchvision resnet18 / resnet50 (restated in oracle/torchvision_restate)
   loss      nn.CrossEntropyLoss (src/training/semi_supervised.py:111) on the
             labelled half + masked CE on the strong view with pseudo-labels
             softmax/max/>=tau (semi_supervised.py:57-66)
@@ -109,10 +109,11 @@ def semi_step_reference(model, opt, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.
 
 
 class CpuSemiStep:
-    def __init__(self, seed: int = 42, tau: float = 0.7, lambda_u: float = 1.0, size: int = 224):
+    def __init__(self, seed: int = 42, tau: float = 0.7, lambda_u: float = 1.0, size: int = 224,
+                 arch: str = "resnet18"):
         torch.manual_seed(seed)
-        self.model = tvm.resnet18()
-        self.model.fc = torch.nn.Linear(512, 2)
+        self.model = getattr(tvm, arch)()
+        self.model.fc = torch.nn.Linear(self.model.fc.in_features, 2)
         self.opt = torch.optim.AdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-4)
         self.tau, self.lambda_u, self.size = tau, lambda_u, size
         self.g = torch.Generator().manual_seed(seed)
@@ -148,18 +149,20 @@ class CpuSemiStep:
 
 
 def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2, threads: int = 16,
-                  seed: int = 0) -> Dict:
-    """Images/sec of the CPU step (the full per-GPU batch,
-    warm-up steps, then the MEDIAN of the timed steps) on a bounded sample of
-    steps x (Bl + Bu) images."""
+                  seed: int = 0, arch: str = "resnet18", size: int = 224, budget_s: float = 0.0) -> Dict:
+    """Images/sec of the CPU step (warm-up steps, then
+    the MEDIAN of the timed steps) on a bounded sample of steps x (Bl + Bu)
+    images of the workload's own architecture and image size.  budget_s > 0
+    stops the timed steps once that much wall time has gone into them (at
+    least 3 are timed); the count actually timed is reported."""
     import statistics
 
     torch.set_num_threads(threads)
     rng = np.random.default_rng(seed)
-    x_l = rng.integers(0, 256, (Bl, 224, 224, 3), dtype=np.uint8)
-    x_u = rng.integers(0, 256, (Bu, 224, 224, 3), dtype=np.uint8)
+    x_l = rng.integers(0, 256, (Bl, size, size, 3), dtype=np.uint8)
+    x_u = rng.integers(0, 256, (Bu, size, size, 3), dtype=np.uint8)
     y_l = torch.from_numpy(rng.integers(0, 2, Bl))
-    step = CpuSemiStep()
+    step = CpuSemiStep(arch=arch, size=size)
     for _ in range(warmup):
         step(x_l, y_l, x_u)
     times = []
@@ -167,8 +170,11 @@ def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2,
         t0 = time.perf_counter()
         step(x_l, y_l, x_u)
         times.append(time.perf_counter() - t0)
+        if budget_s > 0 and len(times) >= 3 and sum(times) >= budget_s:
+            break
     dt = statistics.median(times)
     return {"value": (Bl + Bu) / dt, "step_s": dt, "threads": torch.get_num_threads(), "step_times_s": times,
-            "sample": f"median of {steps} timed steps after {warmup} warm-up, each {Bl} labelled + {Bu} "
-                      f"unlabelled 224x224 uint8 images: PIL weak/strong views + torch fp32 ResNet-18 weak forward "
-                      f"+ joint fwd/bwd + AdamW (oracle/step_oracle.py)"}
+            "steps_timed": len(times), "warmup": warmup,
+            "sample": f"median of {len(times)} timed steps after {warmup} warm-up, each {Bl} labelled + {Bu} "
+                      f"unlabelled {size}x{size} uint8 images: PIL weak/strong views + torch fp32 {arch} weak "
+                      f"forward + joint fwd/bwd + AdamW (oracle/step_oracle.py)"}

@@ -262,65 +262,6 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(int total8, int C, co
   }
 }
 
-// bn_bwd_apply_kernel with 4 channels per thread, bf16 only, held to 64
-// VGPRs (the 8-channel form takes 104) so it runs beside a resident wgrad
-// (see bn_bwd_reduce4_kernel).  Same per-element formula.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
-bn_bwd_apply4_kernel(int total4, int C, const __bf16* __restrict__ dz, const __bf16* __restrict__ zmask,
-                     const uint8_t* __restrict__ mbits, const __bf16* __restrict__ y,
-                     const float* __restrict__ coef, __bf16* __restrict__ dy, __bf16* __restrict__ dpre,
-                     const float* __restrict__ mscale, const float* __restrict__ mshift) {
-  const int cpr = C >> 2;
-  const int start = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c0 = (start % cpr) * 4;
-  const bool amask = mscale != nullptr;
-  const float4 ca = *reinterpret_cast<const float4*>(coef + c0);
-  const float4 cb = *reinterpret_cast<const float4*>(coef + C + c0);
-  const float4 cc = *reinterpret_cast<const float4*>(coef + 2 * C + c0);
-  float4 msc = make_float4(0.f, 0.f, 0.f, 0.f), msh = msc;
-  if (amask) {
-    msc = *reinterpret_cast<const float4*>(mscale + c0);
-    msh = *reinterpret_cast<const float4*>(mshift + c0);
-  }
-  const bf16x4 zero4 = (bf16x4){(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-  const int stride = gridDim.x * blockDim.x;
-  auto one = [&](bf16x4 g, bf16x4 zz, bf16x4 yy, int i) {
-    const float a_[4] = {ca.x, ca.y, ca.z, ca.w}, b_[4] = {cb.x, cb.y, cb.z, cb.w}, c_[4] = {cc.x, cc.y, cc.z, cc.w};
-    const float s_[4] = {msc.x, msc.y, msc.z, msc.w}, h_[4] = {msh.x, msh.y, msh.z, msh.w};
-    const uint32_t mb = mbits ? ((uint32_t)mbits[i >> 1] >> ((i & 1) * 4)) : 0xFu;
-    bf16x4 o, p;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = (float)g[j];
-      const float yv = (float)yy[j];
-      if (zmask) d = (float)zz[j] > 0.f ? d : 0.f;
-      if (amask) d = __builtin_fmaf(yv, s_[j], h_[j]) > 0.f ? d : 0.f;
-      d = ((mb >> j) & 1u) ? d : 0.f;
-      p[j] = (__bf16)d;
-      o[j] = (__bf16)(a_[j] * d + b_[j] * yv + c_[j]);
-    }
-    *reinterpret_cast<bf16x4*>(dy + (long)i * 4) = o;
-    if (dpre) *reinterpret_cast<bf16x4*>(dpre + (long)i * 4) = p;
-  };
-  int i = start;
-  for (; i + stride < total4; i += 2 * stride) {
-    const bf16x4 g0 = *reinterpret_cast<const bf16x4*>(dz + (long)i * 4);
-    const bf16x4 g1 = *reinterpret_cast<const bf16x4*>(dz + (long)(i + stride) * 4);
-    const bf16x4 y0 = *reinterpret_cast<const bf16x4*>(y + (long)i * 4);
-    const bf16x4 y1 = *reinterpret_cast<const bf16x4*>(y + (long)(i + stride) * 4);
-    const bf16x4 z0 = zmask ? *reinterpret_cast<const bf16x4*>(zmask + (long)i * 4) : zero4;
-    const bf16x4 z1 = zmask ? *reinterpret_cast<const bf16x4*>(zmask + (long)(i + stride) * 4) : zero4;
-    one(g0, z0, y0, i);
-    one(g1, z1, y1, i + stride);
-  }
-  if (i < total4) {
-    const bf16x4 g0 = *reinterpret_cast<const bf16x4*>(dz + (long)i * 4);
-    const bf16x4 y0 = *reinterpret_cast<const bf16x4*>(y + (long)i * 4);
-    const bf16x4 z0 = zmask ? *reinterpret_cast<const bf16x4*>(zmask + (long)i * 4) : zero4;
-    one(g0, z0, y0, i);
-  }
-}
-
 // Backward of z = relu(BN_a(ya) + BN_b(yb)): dout = dz * (zmask > 0) is the
 // gradient of both BN outputs.  Per-(row block, channel) sums of dout,
 // dout*xhat_a and dout*xhat_b, written as two [C][blocks][2] partial sets
@@ -500,12 +441,8 @@ int ssip_bn_finalize(int C, int tiles, float* partial, const float* gamma, const
                    mean_out, invstd_out, scale_out, shift_out};
   const int S = fin_splits(tiles);
   double* scratch = fin_scratch(partial, (int64_t)C * tiles * 3);
-  if (fin_nt() == 64)
-    hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3(S, C), dim3(64), 0, st, C, tiles, S, (const float*)partial,
-                       scratch, f);
-  else
-    hipLaunchKernelGGL(bn_finalize_kernel<256>, dim3(S, C), dim3(256), 0, st, C, tiles, S, (const float*)partial,
-                       scratch, f);
+  hipLaunchKernelGGL(bn_finalize_kernel<FIN_NT>, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S,
+                     (const float*)partial, scratch, f);
   if (S > 1)
     hipLaunchKernelGGL(bn_finalize_merge_kernel, dim3((C + FIN_NT / 64 - 1) / (FIN_NT / 64)), dim3(FIN_NT), 0, st,
                        C, S, (const double*)scratch, f);
@@ -614,29 +551,17 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   const int blocks = (int)((M + rows - 1) / rows);
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_bwd: unsupported size");
   const int total8 = (int)(M * C / 8);
-  // SSIP_BWD_REDUCE4=1 / SSIP_BWD_APPLY4=1: the 64-VGPR 4-channel forms (opt-in:
-  // running beside the wgrads they made the step slower, 6.70 vs 6.50 ms)
-  static const bool red4 = getenv("SSIP_BWD_REDUCE4") && atoi(getenv("SSIP_BWD_REDUCE4")) != 0;
-  static const bool apply4 = getenv("SSIP_BWD_APPLY4") && atoi(getenv("SSIP_BWD_APPLY4")) != 0;
+  // (64-VGPR 4-channel forms that fit beside a resident wgrad made the step
+  // slower, 6.70 vs 6.50 ms: r3-variants branch)
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    if (sizeof(T) == 2 && red4 && C / 4 <= 256 && 256 % (C / 4) == 0)
-      hipLaunchKernelGGL(bn_bwd_reduce4_kernel, dim3(blocks), dim3(256), 0, st, (long)M, C, rows,
-                         (const __bf16*)dz, (const __bf16*)zmask, mbits, (const __bf16*)y, mean, invstd, mscale,
-                         mshift, partial);
-    else
-      hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
-                         (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
+                       (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
     BnBwdFin f;
     f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
                               fin_scratch(partial, (int64_t)blocks * C * 2));
     launch_bn_bwd_finalize(st, C, blocks, (long)M, 1, 1, f, accumulate);
-    if (sizeof(T) == 2 && apply4 && C / 4 <= 256 && 256 % (C / 4) == 0 && M * C / 4 < (1l << 31))
-      hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(bn_elem_grid(2 * (long)total8)), dim3(256), 0, st,
-                         (int)(2 * (long)total8), C, (const __bf16*)dz, (const __bf16*)zmask, mbits,
-                         (const __bf16*)y, coef, (__bf16*)dy, (__bf16*)dpre, mscale, mshift);
-    else
-      hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
-                         (const T*)dz, (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
+                       (const T*)dz, (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
 }

@@ -133,12 +133,8 @@ __global__ void __launch_bounds__(FIN_NT) bn_bwd_finalize_merge_kernel(int C, in
 static inline void launch_bn_bwd_finalize(hipStream_t st, int C, int blocks, long M, int cmajor, int sets,
                                           const BnBwdFin& fin, int accumulate) {
   const int S = fin_splits(blocks);
-  if (fin_nt() == 64)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<64>, dim3(S, sets * C), dim3(64), 0, st, C, blocks, S, M, cmajor, fin,
-                       accumulate);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<256>, dim3(S, sets * C), dim3(256), 0, st, C, blocks, S, M, cmajor,
-                       fin, accumulate);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<FIN_NT>, dim3(S, sets * C), dim3(FIN_NT), 0, st, C, blocks, S, M,
+                     cmajor, fin, accumulate);
   if (S > 1)
     hipLaunchKernelGGL(bn_bwd_finalize_merge_kernel, dim3((sets * C + FIN_NT / 64 - 1) / (FIN_NT / 64)),
                        dim3(FIN_NT), 0, st, C, sets, S, M, fin, accumulate);
@@ -283,119 +279,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(long M, int C, int r
   }
 }
 
-// The same sums with 4 channels per thread, bf16 only, held to 64 VGPRs so
-// a workgroup fits beside a resident wgrad (2 workgroups of 8 waves at <= 112
-// VGPRs per CU leave 64 per SIMD lane slot): in the train step the 8-channel
-// form (163 VGPRs) could start only as wgrad workgroups retired, 2-4x its
-// isolated time.  Rows walk in the same r += rpi order (rpi = 256 / (C / 4));
-// the totals are combined like chunk_sums (butterfly, <= 4 LDS groups).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
-bn_bwd_reduce4_kernel(long M, int C, int rows_per_block, const __bf16* __restrict__ dz,
-                      const __bf16* __restrict__ zmask, const uint8_t* __restrict__ mbits,
-                      const __bf16* __restrict__ y, const float* __restrict__ mean,
-                      const float* __restrict__ invstd, const float* __restrict__ mscale,
-                      const float* __restrict__ mshift, float* __restrict__ partial) {
-  const int cpr = C / 4;  // 4-channel chunks per row
-  const int rpi = 256 / cpr;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int chunk = tid % cpr, rsub = tid / cpr;
-  const int c0 = chunk * 4;
-  const long r0 = (long)blockIdx.x * rows_per_block;
-  const long r1 = min(r0 + rows_per_block, M);
-  const bool amask = mscale != nullptr;
-  float sd[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
-  const float4 mu = *reinterpret_cast<const float4*>(mean + c0);
-  const float4 is = *reinterpret_cast<const float4*>(invstd + c0);
-  float4 msc = make_float4(0.f, 0.f, 0.f, 0.f), msh = msc;
-  if (amask) {
-    msc = *reinterpret_cast<const float4*>(mscale + c0);
-    msh = *reinterpret_cast<const float4*>(mshift + c0);
-  }
-  const int mshift_bits = (chunk & 1) * 4;
-  const int cpr8 = C / 8;
-  auto acc = [&](bf16x4 g, bf16x4 zz, uint32_t mb, bf16x4 yy) {
-    const float m_[4] = {mu.x, mu.y, mu.z, mu.w}, i_[4] = {is.x, is.y, is.z, is.w};
-    const float a_[4] = {msc.x, msc.y, msc.z, msc.w}, b_[4] = {msh.x, msh.y, msh.z, msh.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = (float)g[j];
-      const float yv = (float)yy[j];
-      if (zmask) d = (float)zz[j] > 0.f ? d : 0.f;
-      if (amask) d = __builtin_fmaf(yv, a_[j], b_[j]) > 0.f ? d : 0.f;
-      d = ((mb >> j) & 1u) ? d : 0.f;
-      sd[j] += d;
-      sx[j] += d * ((yv - m_[j]) * i_[j]);
-    }
-  };
-  if (rsub < rpi) {
-    constexpr int U = 1;
-    const bf16x4 z0 = (bf16x4){(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
-    long r = r0 + rsub;
-    for (; r + (U - 1) * rpi < r1; r += U * rpi) {
-      bf16x4 g[U], z[U], yv[U];
-      uint32_t mb[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long rr = r + (long)u * rpi;
-        g[u] = *reinterpret_cast<const bf16x4*>(dz + rr * C + c0);
-        yv[u] = *reinterpret_cast<const bf16x4*>(y + rr * C + c0);
-        z[u] = zmask ? *reinterpret_cast<const bf16x4*>(zmask + rr * C + c0) : z0;
-        mb[u] = mbits ? ((uint32_t)mbits[rr * cpr8 + (chunk >> 1)] >> mshift_bits) : 0xFu;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) acc(g[u], z[u], mb[u], yv[u]);
-    }
-    for (; r < r1; r += rpi) {
-      const bf16x4 g = *reinterpret_cast<const bf16x4*>(dz + r * C + c0);
-      const bf16x4 yy = *reinterpret_cast<const bf16x4*>(y + r * C + c0);
-      const bf16x4 zz = zmask ? *reinterpret_cast<const bf16x4*>(zmask + r * C + c0) : z0;
-      const uint32_t mb = mbits ? ((uint32_t)mbits[r * cpr8 + (chunk >> 1)] >> mshift_bits) : 0xFu;
-      acc(g, zz, mb, yy);
-    }
-  }
-  // totals over the threads sharing a chunk: butterfly over the lane bits
-  // above log2(cpr), then <= 4 groups through LDS in fixed order
-  __shared__ float red[256][9];
-  if (cpr < 64) {
-    for (int o = cpr; o < 64; o <<= 1)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sd[j] += __shfl_xor(sd[j], o, 64);
-        sx[j] += __shfl_xor(sx[j], o, 64);
-      }
-  }
-  const int groups = cpr < 64 ? 4 : 256 / cpr;
-  const bool writer = cpr < 64 ? lane < cpr : true;
-  const int slot = cpr < 64 ? (tid >> 6) * cpr + lane : tid;
-  if (writer)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      red[slot][j] = sd[j];
-      red[slot][4 + j] = sx[j];
-    }
-  __syncthreads();
-  if (tid < cpr) {
-    float* out = partial + ((long)c0 * gridDim.x + blockIdx.x) * 2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float a = 0.f, b = 0.f;
-      for (int g = 0; g < groups; ++g) {
-        a += red[g * cpr + tid][j];
-        b += red[g * cpr + tid][4 + j];
-      }
-      out[(long)j * gridDim.x * 2] = a;
-      out[(long)j * gridDim.x * 2 + 1] = b;
-    }
-  }
-}
-
 static inline int bwd_rows_per_block(long M, int C) {
   // aim for ~512 blocks (2 per CU), at least eight iterations of rows (fewer,
   // longer blocks: 38.1 vs 43.8 us at layer1 batch 256, 15.6 vs 19.5 at layer3,
   // tools/time_bn_bwd.py)
-  // (SSIP_BWD_BLOCKS / SSIP_BWD_ITERS: tuning overrides)
-  static const long nb = getenv("SSIP_BWD_BLOCKS") ? atol(getenv("SSIP_BWD_BLOCKS")) : 512;
-  static const long it = getenv("SSIP_BWD_ITERS") ? atol(getenv("SSIP_BWD_ITERS")) : 8;
+  constexpr long nb = 512, it = 8;
   const int rpi = 256 / (C / 8);
   long rows = (M + nb - 1) / nb;
   if (rows < it * rpi) rows = it * rpi;

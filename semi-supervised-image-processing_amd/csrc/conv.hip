@@ -917,14 +917,12 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 // 64-deep k-step covers filter rows 2ks and 2ks+1; k >= R*S*4 reads zeros.
 // POST: DGRAD with the BN-backward epilogue (ssip_conv_dgrad_bn); its
 // operand registers are only allocated in that instantiation.
-// LDIAG (timing experiments only, SSIP_LOOP_DIAG; results are wrong): 2-stage
-// k-loop with 1 = no MFMAs, 2 = no fragment reads, 4 = no LDS-DMA issue,
-// 8 = no barrier
+// (Round 3's timing ablations of this k-loop, its 5- and 8-phase ping-pong
+// schedules and the persistent row-balanced halo kernel conv_hb -- all
+// measured no faster in the step -- live on the r3-variants branch.)
 template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false,
-          bool FOLD = false, int LDIAG = 0>
-__global__ void __launch_bounds__(64 * WMW * WNW,
-                                  (NSTAGE == 5 || NSTAGE == 8) ? 2
-                                                                : glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
+          bool FOLD = false>
+__global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
     conv_glds_kernel(const ConvArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, BK = 64;
@@ -934,15 +932,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   constexpr int A_BYTES = WG ? BK * BM * 2 : BM * 128;
   constexpr int B_BYTES = WG ? BK * BN * 2 : BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  // NSTAGE 5 = the ping-pong schedule on two LDS buffers (see the main loop)
-  static_assert(NSTAGE == 2 || NSTAGE == 3 || NSTAGE == 5 || NSTAGE == 8, "2 or 3 LDS stages, or ping-pong");
-  constexpr bool PP = NSTAGE == 5;
-  // NSTAGE 8 = the 8-phase ping-pong schedule for 256x256 tiles (see the main loop)
-  constexpr bool PP8 = NSTAGE == 8;
-  static_assert(!PP8 || (BM == 256 && BN == 256 && WMW == 2 && WNW == 4 && !C4 && !POST),
-                "the 8-phase schedule is built for 256x256 FWD / stride-1 DGRAD / WGRAD tiles of 8 waves (2 x 4)");
-  constexpr int NBUF = (PP || PP8) ? 2 : NSTAGE;
-  static_assert(!PP || (NW == 8 && !POST), "ping-pong pairs the 8 waves of a workgroup two per SIMD");
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "2 or 3 LDS stages");
+  constexpr int NBUF = NSTAGE;
   constexpr int IA = A_BYTES / 1024, IB = B_BYTES / 1024;
   constexpr int LA = IA / NW, LB = IB / NW;
   constexpr int L = LA + LB;
@@ -1109,22 +1100,12 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
       const int lc = (lane % CPB) ^ (MTile<T, BN>::swz(row) >> 1);
       const int col = n0 + lc * 8;
       b_row[t] = row;
-      if constexpr (PP8) {
-        // C % 256 == 0 (host): the 256 columns of a tile are one tap, so the
-        // tap and its valid p / q ranges are workgroup-uniform (scalars)
-        const int rs = n0 / a.C;
-        b_ok[t] = true;
-        b_c[t] = n0 - rs * a.C + lc * 8;
-        b_r[t] = rs / a.S;
-        b_s[t] = rs - b_r[t] * a.S;
-      } else {
-        b_ok[t] = col < a.Ng;
-        const int cc = b_ok[t] ? col : 0;
-        const int rs = cc / a.C;
-        b_c[t] = cc - rs * a.C;
-        b_r[t] = rs / a.S;
-        b_s[t] = rs - b_r[t] * a.S;
-      }
+      b_ok[t] = col < a.Ng;
+      const int cc = b_ok[t] ? col : 0;
+      const int rs = cc / a.C;
+      b_c[t] = cc - rs * a.C;
+      b_r[t] = rs / a.S;
+      b_s[t] = rs - b_r[t] * a.S;
     }
   }
 
@@ -1174,15 +1155,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   // for which that tap lies inside the image (fixed: the slot's tap is fixed)
   int w_p[LB], w_q[LB], w_plo[LB], w_pn[LB], w_qlo[LB], w_qn[LB];
   uint32_t w_pix[LB];
-  int u_plo = 0, u_pn = 0, u_qlo = 0, u_qn = 0;  // PP8 WGRAD: the tile's (uniform) tap ranges
-  if constexpr (WG && PP8) {
-    const int rs = n0 / a.C, ur = rs / a.S, us = rs - ur * a.S;
-    const int r0 = a.pad - ur, s0 = a.pad - us;
-    u_plo = r0 > 0 ? (r0 + a.stride - 1) / a.stride : 0;
-    u_pn = max(0, min(a.P, (a.H - 1 + r0) >= 0 ? (a.H - 1 + r0) / a.stride + 1 : 0) - u_plo);
-    u_qlo = s0 > 0 ? (s0 + a.stride - 1) / a.stride : 0;
-    u_qn = max(0, min(a.Q, (a.W - 1 + s0) >= 0 ? (a.W - 1 + s0) / a.stride + 1 : 0) - u_qlo);
-  } else if constexpr (WG) {
+  if constexpr (WG) {
 #pragma unroll
     for (int t = 0; t < LB; ++t) {
       const int m = (int)min(mstart + b_row[t], (long)a.Mred - 1);
@@ -1317,274 +1290,13 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
   // fused-BN epilogue operands: issued first, landed long before the epilogue
   BnPostRegs<T, BM, BN, 64 * WMW * WNW> post;
   if constexpr (MODE == MODE_DGRAD && POST) post.load(a, m0, n0);
-  if constexpr (PP8) {
-    // 8-phase ping-pong (cdna_hip_programming.md, "The 256^2 8-phase template"):
-    // waves 0-3 (group 0, rows 0-127) and 4-7 (group 1, rows 128-255; one of
-    // each group per SIMD) run the same phases one barrier apart, so in every
-    // barrier interval one wave per SIMD reads fragments / issues LDS-DMA while
-    // its partner runs 16 MFMAs.  A k-step is 4 phases, one C quadrant each:
-    // (rows 0-63, cols 0-31) (0-63, 32-63) (64-127, 32-63) (64-127, 0-31) of the
-    // wave's 128x64 tile; A fragments are re-read every second phase, B every
-    // phase, so 48 VGPRs hold the operands.
-    // Two LDS buffers (k-step parity), each split into an A and a B region.
-    // Loads run ahead per region: B of k-step t+1 is issued in phase 0 of t
-    // (its region was last read in phase 3 of t-1), A of t+2 in phase 3 of t
-    // (its region was last read in phase 2 of t).  Every phase retires its own
-    // fragment reads (lgkmcnt(0)) before its first barrier, so a region is free
-    // for DMA once the barrier after its last read has passed.  All of k-step
-    // t+1's loads are retired by a counted vmcnt (only A of t+2 stays in flight)
-    // before the barrier that precedes the first read of t+1.
-    const int g = wave >> 2;
-    int nk = ph_ksteps;
-    if constexpr (WG) {
-      const long rem = mend - mstart;
-      nk = rem > 0 ? (int)((rem + BK - 1) / BK) : 0;
-    }
-    int kr_a = 0, ks_a = 0, kcb_a = 0;  // k-position of the next A k-step issued
-    int ks_next_a = 0;  // WGRAD: k-step of the next A issue
-    auto issueA = [&](int stage) {
-      char* As = smem + stage * STAGE;
-      if constexpr (WG) {  // dY rows of the k-step (m-major)
-        const int ks = ks_next_a++;
-        const int mlim = (int)(mend - mstart) - ks * BK;
-        const uint32_t moff = (uint32_t)(ks * BK * a.K * 2);
-        constexpr int CPA = BM / 8, RPA = 64 / CPA;
-#pragma unroll
-        for (int t = 0; t < LA; ++t) {  // K % 256 == 0 (host): every column is inside
-          const int row = RPA * (wave + NW * t) + lane / CPA;
-          // rows of slot t are row_0 + RPA * NW * t, same swizzle: one offset register
-          blds16(rsA, row < mlim ? a_off[0] + (uint32_t)(RPA * NW * t * a.K * 2) + moff : SSIP_OOB,
-                 As + (wave + NW * t) * 1024);
-        }
-        return;
-      }
-      uint32_t toff;
-      int tp;
-      if constexpr (MODE == MODE_FWD) {
-        tp = kr_a * a.S + ks_a;
-        toff = (uint32_t)(((kr_a * a.W + ks_a) * a.C + kcb_a) * 2);
-      } else {
-        tp = kr_a * ph_ns + ks_a;
-        toff = (uint32_t)((kcb_a - (kr_a * a.Q + ks_a) * a.K) * 2);
-      }
-#pragma unroll
-      for (int t = 0; t < LA; ++t) {
-        const bool ok = (a_msk[t] >> tp) & 1u;
-        blds16(rsA, ok ? a_off[t] + toff : SSIP_OOB, As + (wave + NW * t) * 1024);
-      }
-      kcb_a += BK;
-      if (kcb_a >= Cred) {
-        kcb_a = 0;
-        if (++ks_a >= ph_ns) { ks_a = 0; ++kr_a; }
-      }
-    };
-    auto issueB = [&](int ks, int stage) {
-      char* Bs = smem + stage * STAGE + A_BYTES;
-      if constexpr (WG) {  // im2col rows of x, each slot walked one k-step on (calls come in k order)
-        const int mlim = (int)(mend - mstart) - ks * BK;
-        constexpr int CPB = BN / 8, RPB = 64 / CPB;
-        // the slot's output pixel recomputed per k-step (no per-slot walk state:
-        // the 128 accumulators leave no registers for it); tap and channel
-        // chunk are the same for every slot (b_c[0]: rows 16 apart share a swizzle)
-        const int rs = n0 / a.C, ur = rs / a.S, us = rs - ur * a.S;
-#pragma unroll
-        for (int t = 0; t < LB; ++t) {
-          const int row = RPB * (wave + NW * t) + lane / CPB;
-          const int m = min((int)mstart + ks * BK + row, a.Mred - 1);
-          const int n = fdiv(m, a.div_pq);
-          const int rem = m - n * a.P * a.Q;
-          const int pp = fdiv(rem, a.div_q);
-          const int qq = rem - pp * a.Q;
-          const bool ok = row < mlim && (uint32_t)(pp - u_plo) < (uint32_t)u_pn &&
-                          (uint32_t)(qq - u_qlo) < (uint32_t)u_qn;
-          const int hin = pp * a.stride - a.pad + ur, win = qq * a.stride - a.pad + us;
-          const uint32_t pix = (uint32_t)(((n * a.H + hin) * a.W + win) * a.C + b_c[0]) * 2u;
-          blds16(rsB, ok ? pix : SSIP_OOB, Bs + (wave + NW * t) * 1024);
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < LB; ++t) blds16(rsB, b_off[t] + (uint32_t)(ks * BK * 2), Bs + (wave + NW * t) * 1024);
-      }
-    };
-    Frag<T> fa[2][4], fb[2][2];
-    auto readA = [&](int buf, int mi) {
-      const char* As = smem + buf * STAGE;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if constexpr (WG) read_mfrag<BM>(fa[h][i], As, wm * 128 + (mi * 4 + i) * 16, lane, h);
-          else read_kfrag(fa[h][i], As, wm * 128 + (mi * 4 + i) * 16 + (lane & 15), lane >> 4, h);
-        }
-    };
-    auto readB = [&](int buf, int nj) {
-      const char* Bs = smem + buf * STAGE + A_BYTES;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if constexpr (WG) read_mfrag<BN>(fb[h][j], Bs, wn * 64 + (nj * 2 + j) * 16, lane, h);
-          else read_kfrag(fb[h][j], Bs, wn * 64 + (nj * 2 + j) * 16 + (lane & 15), lane >> 4, h);
-        }
-    };
-#define SSIP_PP8_MFMA(MI, NJ)                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                              \
-    __builtin_amdgcn_s_setprio(1);                                                  \
-    _Pragma("unroll") for (int h = 0; h < 2; ++h)                                   \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                   \
-    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                   \
-        mma(acc[(MI) * 4 + i][(NJ) * 2 + j], fa[h][i], fb[h][j]);                   \
-    __builtin_amdgcn_s_setprio(0);                                                  \
-    __builtin_amdgcn_sched_barrier(0);
-#define SSIP_PP8_SYNC(ASM)                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                              \
-    asm volatile(ASM ::: "memory");                                                 \
-    __builtin_amdgcn_sched_barrier(0);
-    if (nk > 0) {
-      issueA(0);
-      issueB(0, 0);
-      if (nk > 1) {
-        issueA(1);
-        wait_vm_barrier<LA>();
-      } else {
-        wait_vm_barrier<0>();
-      }
-      if (g) { SSIP_PP8_SYNC("s_barrier") }
-      for (int t = 0; t < nk; ++t) {
-        const int buf = t & 1;
-        // phase 0: quadrant (0, 0); B of k-step t+1 into the other buffer
-        readA(buf, 0);
-        readB(buf, 0);
-        if (t + 1 < nk) issueB(t + 1, buf ^ 1);
-        SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
-        SSIP_PP8_MFMA(0, 0)
-        SSIP_PP8_SYNC("s_barrier")
-        // phase 1: (0, 1)
-        readB(buf, 1);
-        SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
-        SSIP_PP8_MFMA(0, 1)
-        SSIP_PP8_SYNC("s_barrier")
-        // phase 2: (1, 1)
-        readA(buf, 1);
-        SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
-        SSIP_PP8_MFMA(1, 1)
-        SSIP_PP8_SYNC("s_barrier")
-        // phase 3: (1, 0); A of k-step t+2 into this buffer's A region; k-step
-        // t+1 retired (counted) before the barrier that ends this phase for
-        // both groups (group 1: its first barrier, group 0: its second)
-        readB(buf, 0);
-        const bool more = t + 2 < nk;
-        if (more) issueA(buf);
-        if (g) {
-          if (more) { SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(4)\n\ts_barrier") }
-          else { SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)\n\ts_barrier") }
-          SSIP_PP8_MFMA(1, 0)
-          SSIP_PP8_SYNC("s_barrier")
-        } else {
-          SSIP_PP8_SYNC("s_waitcnt lgkmcnt(0)\n\ts_barrier")
-          SSIP_PP8_MFMA(1, 0)
-          if (more) { SSIP_PP8_SYNC("s_waitcnt vmcnt(4)\n\ts_barrier") }
-          else { SSIP_PP8_SYNC("s_waitcnt vmcnt(0)\n\ts_barrier") }
-        }
-      }
-      if (!g) { SSIP_PP8_SYNC("s_barrier") }
-    }
-#undef SSIP_PP8_MFMA
-#undef SSIP_PP8_SYNC
-    static_assert(!PP8 || LA == 4, "vmcnt(4) above counts one k-step of A loads per wave");
-  } else if constexpr (PP) {
-    // Ping-pong (MI355X_MICROARCH.md "Two waves per SIMD"): waves 0-3
-    // (group 0) and 4-7 (group 1; one on each SIMD beside a group-0 wave)
-    // run the same k-steps one barrier interval apart, so in every interval
-    // one wave of each SIMD reads fragments while its partner runs MFMAs.
-    // Interval 2s: group 0 reads k-step s and issues its share of k-step s+1
-    // (into the buffer both groups finished reading before the interval);
-    // group 1 runs the MFMAs of s-1 and issues its share of s+1.
-    // Interval 2s+1: group 0 runs the MFMAs of s; group 1 reads s.  Every
-    // wave retires its own LDS-DMA with vmcnt(0) at the end of interval
-    // 2s+1, before the barrier after which k-step s+1 is first read.
-    const bool g1 = wave >= NW / 2;
-    Frag<T> fa[2][FM], fb[2][FN];
-    auto read_all = [&](int buf) {
-      const char* As = smem + buf * STAGE;
-      const char* Bs = As + A_BYTES;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if constexpr (!WG) {
-#pragma unroll
-          for (int i = 0; i < FM; ++i) read_kfrag(fa[h][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, h);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) read_kfrag(fb[h][j], Bs, wn * WTN + j * 16 + (lane & 15), lane >> 4, h);
-        } else {
-#pragma unroll
-          for (int i = 0; i < FM; ++i) read_mfrag<BM>(fa[h][i], As, wm * WTM + i * 16, lane, h);
-#pragma unroll
-          for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[h][j], Bs, wn * WTN + j * 16, lane, h);
-        }
-      }
-    };
-    auto mfma_all = [&]() {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    if (nsteps > 0) {
-      issue(0, 0);
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      if (g1) {  // interval 0 of group 1: no MFMAs yet, only its share of k-step 1
-        if (nsteps > 1) issue(1, 1);
-        asm volatile("s_barrier" ::: "memory");
-      }
-      for (int ks = 0; ks < nsteps; ++ks) {
-        const int buf = ks & 1;
-        if (!g1) {
-          read_all(buf);
-          if (ks + 1 < nsteps) issue(ks + 1, buf ^ 1);
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_all();
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        } else {
-          read_all(buf);
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_all();
-          if (ks + 2 < nsteps) issue(ks + 2, buf);
-          __builtin_amdgcn_sched_barrier(0);
-          asm volatile("s_barrier" ::: "memory");
-        }
-      }
-      if (!g1) asm volatile("s_barrier" ::: "memory");
-    }
-  } else {
   if (nsteps > 0) issue(0, 0);
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
   Frag<T> fa[2][FM], fb[2][FN];
-  if constexpr ((LDIAG & 2) != 0) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) read_kfrag(fa[h][i], smem, i * 16 + (lane & 15), lane >> 4, h);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) read_kfrag(fb[h][j], smem, j * 16 + (lane & 15), lane >> 4, h);
-    }
-  }
   for (int ks = 0; ks < nsteps; ++ks) {
-    if constexpr ((LDIAG & 8) != 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
-    }
-    if constexpr ((LDIAG & 4) == 0) {
-      if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
-    }
+    if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
+    if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
     const char* As = smem + stage * STAGE;
     const char* Bs = As + A_BYTES;
     // both k-halves' fragments are requested before the first MFMA, so the
@@ -1593,7 +1305,6 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
     constexpr bool BOTH = FM + FN <= 8;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if ((LDIAG & 2) != 0) break;
       if (!BOTH && h == 1) break;
       if constexpr (!WG) {
 #pragma unroll
@@ -1609,7 +1320,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if ((LDIAG & 2) == 0 && !BOTH && h == 1) {
+      if (!BOTH && h == 1) {
         if constexpr (!WG) {
 #pragma unroll
           for (int i = 0; i < FM; ++i) read_kfrag(fa[1][i], As, wm * WTM + i * 16 + (lane & 15), lane >> 4, 1);
@@ -1622,21 +1333,13 @@ __global__ void __launch_bounds__(64 * WMW * WNW,
           for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[1][j], Bs, wn * WTN + j * 16, lane, 1);
         }
       }
-      if constexpr ((LDIAG & 1) != 0) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(fa[h][i].v));
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(fb[h][j].v));
-      } else {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
-      }
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
     }
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
-  }  // !PP
   __syncthreads();
   if constexpr (MODE == MODE_DGRAD && POST)
     conv_epilogue<MODE, T, BM, BN, WMW, WNW>(a, acc, smem, m0, n0, tm, post, rmap, by);
@@ -1796,7 +1499,6 @@ struct HaloArgs {
   int relu;           // FWD ReLU after bias and residual
   uint32_t x_bytes, w_bytes, o_bytes;
   int N, H, W, Ncols, TR, tiles, units, flip;
-  int dbg;  // ablation (tools/time_halo.py): 1 = no MFMA, 2 = no epilogue
   // DGRAD BN-backward post-op (conv_halo_kernel<..., BNPOST>, ssip_conv_dgrad_bn):
   // out = (dgrad + add) * relu_mask, and per-(channel, workgroup, wave row)
   // sums {out, out * (y - mean) * invstd} into partial [Ncols][G][HALO_WMW][2].
@@ -2041,29 +1743,18 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
       for (int jj = 0; jj < FN; ++jj) rb[jj].v = *reinterpret_cast<const bf16x8*>(bt + boff[jj][kh]);
     };
-    if (a.dbg != 1) {
-      load_step(0, fa[0], fb[0]);
+    load_step(0, fa[0], fb[0]);
 #pragma unroll
-      for (int st = 0; st < 18; ++st) {
-        if (st + 1 < 18) load_step(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+    for (int st = 0; st < 18; ++st) {
+      if (st + 1 < 18) load_step(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
-      }
+        for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
     }
     // the next tile's rows (issued before the MFMAs) and this wave's older
     // stores retire here; nothing younger is in flight
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (a.dbg == 2) {
-      if (more && !prefetch) {
-        halo_lds_barrier();
-        issue_w(jn_next);
-        issue_x(un - jn_next * a.tiles, Xn);
-        first = true;
-      }
-      continue;
-    }
 
     // ---- epilogue
     if constexpr (BNPOST) {
@@ -2172,352 +1863,6 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
       first = true;
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// Row-balanced halo kernel (hb): 3x3 / stride 1 / pad 1 FWD and stride-1
-// DGRAD over >= 128 reduction channels (ResNet layers 2-4).
-//
-// Why (profiles/r3_loop_diag.txt): the implicit-GEMM ring kernel stages every
-// tap's A rows through LDS-DMA, so each input pixel crosses L2 -> LDS nine
-// times; at 128x128 tiles that is 15.6 B of DMA per kFLOP, and the per-CU
-// LDS-DMA intake (~68 GB/s) alone takes longer than the MFMAs (l3 fwd: DMA +
-// barrier only 53.7 us of a 73.9 us kernel).  Here the A operand of a 64-
-// channel chunk is one zero-haloed image of the tile's input rows, DMA'd
-// once for the chunk's nine taps (tap (r, s) of output pixel (n, p, q) is LDS
-// pixel base(n, p, q) + r (W+2) + s, as in conv_halo_kernel); only the
-// weights stream per k-step.  256 x BN tiles: ~5 B of DMA per kFLOP.
-//
-// Decomposition: one persistent workgroup per CU takes an equal contiguous
-// range of (column block, output pixel) units, cut into tiles of <= 256
-// pixels (ragged ends allowed: any pixel range has a halo window), so every
-// CU does the same MFMA work -- no wave-quantisation tail (layer 3 at batch
-// 256: 196 output rows per CU instead of 196 256x256 tiles on 256 CUs).
-//
-// k-loop: 9 taps x (Cr / 64) chunks, chunk-major; per k-step a counted wait +
-// barrier, then the next k-step's weights (2-stage ring) and, at a chunk's
-// first k-step, the next chunk's input window (2 buffers; the next tile's
-// first chunk during the tile's last) are issued before the MFMAs.
-// Epilogue as conv_halo_kernel: 16-bit stores from the accumulators (+ the
-// residual-gradient add for DGRAD), FWD BatchNorm records [Ncols][G][HALO_WMW][3]
-// per (channel, workgroup, wave row).  The k-order (chunk-major) differs from
-// conv_glds_kernel's (tap-major), so outputs agree to fp32 rounding.
-// ---------------------------------------------------------------------------
-struct HbArgs {
-  const __bf16* X;    // [N][H][W][Cr]  (FWD: x, DGRAD: dy)
-  const __bf16* Wt;   // [Ncols][9][Cr] (FWD: w_krsc, DGRAD: w_crsk)
-  __bf16* out;        // [N][H][W][Ncols]
-  const __bf16* add;  // DGRAD residual gradient (nullable, may alias out)
-  float* partial;     // FWD BN records (nullable)
-  uint32_t x_bytes, w_bytes, o_bytes;
-  int N, H, W, Cr, Ncols, M;
-  int lxw;            // log2 of the LDS image's row pitch XW >= W + 2 (pixels)
-  FastDiv div_hp;     // / (H + 2)
-  long units;         // M * (Ncols / BN)
-  int tm;             // output pixels per tile (<= HB_TM; the host's choice keeps every window in HB_XBUF)
-  int dbg;            // timing ablations (tools): 1 = no MFMA, 2 = every wave multiplies all its fragments
-};
-
-constexpr int HB_XBUF = 56 * 1024;  // one input window: <= 448 pixels x 128 B (host-checked)
-constexpr int HB_TM = 256;          // output pixels per tile
-
-// input window of the tile [m0, m0 + rows): padded rows n (H+2) + p + 1 of
-// input row p = -1 .. H of image n, from the first output row's p - 1 to the
-// last one's p + 1; LDS rows of XW = 2^lxw pixels (a power of two >= W + 2, so
-// a tap's row shift r XW keeps every pixel's swizzle phase)
-__device__ __forceinline__ void hb_window(const HbArgs& a, int m0, int rows, int& pr_lo, int& npx) {
-  const int HW = a.H * a.W, Hp = a.H + 2;
-  const int n0 = m0 / HW, p0 = (m0 - n0 * HW) / a.W;
-  const int m1 = m0 + rows - 1;
-  const int n1 = m1 / HW, p1 = (m1 - n1 * HW) / a.W;
-  pr_lo = n0 * Hp + p0;
-  npx = min((n1 * Hp + p1 + 3 - pr_lo) << a.lxw, HB_XBUF / 128);
-}
-
-template <int BN, int WNW, bool FLIP>
-__global__ void __launch_bounds__(256 * WNW, 1) conv_hb_kernel(const HbArgs a) {
-  typedef __bf16 T;
-  constexpr int WMW = 4, NW = WMW * WNW, NT = 64 * NW;
-  constexpr int WTM = HB_TM / WMW, WTN = BN / WNW, FM = WTM / 16, FN = WTN / 16;
-  constexpr int B_BYTES = BN * 128;
-  constexpr int NWI = NW;  // every wave issues its share of the LDS-DMA
-  constexpr int IB = B_BYTES / 1024, LB = IB / NWI;  // weight DMA instructions per k-step / per issuing wave
-  constexpr int NXW = HB_XBUF / 1024 / NWI;          // window DMA instructions per chunk / per issuing wave (fixed)
-  constexpr int NSB = 3;                             // weight ring: k-steps ks+1, ks+2 in flight during ks
-  static_assert(IB % NWI == 0 && LB >= 1 && FM == 4 && FN >= 1 && WMW <= HALO_WMW && HB_XBUF % (1024 * NWI) == 0,
-                "hb tile");
-  static_assert(NSB * B_BYTES + 2 * HB_XBUF <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NSB * B_BYTES + 2 * HB_XBUF];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // waves w and w + 4 share a SIMD: pair wave rows (0, 3) and (1, 2), so a
-  // ragged tile (rows filling wave rows 0, 1, ... in order) loads the SIMDs evenly
-  static_assert(WNW == 2, "the SIMD pairing below assumes 4 x 2 waves");
-  const int wm = wave < 4 ? (wave >> 1) : 3 - ((wave - 4) >> 1), wn = wave & 1;
-  const int G = gridDim.x, g = blockIdx.x;
-  const long u0 = (long)g * a.units / G, u1 = (long)(g + 1) * a.units / G;
-  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsW = make_rsrc(a.Wt, a.w_bytes);
-  const __amdgpu_buffer_rsrc_t rsO = make_rsrc(a.out, a.o_bytes), rsA = make_rsrc(a.add, a.o_bytes);
-  const int Hp = a.H + 2, HW = a.H * a.W, XW = 1 << a.lxw;
-  const int nc = a.Cr / 64;
-  const int kq = lane >> 4;
-  const long M = a.M;
-
-  // BN records [Ncols][G][HALO_WMW][3]: zero this workgroup's (the k-loop's
-  // vmcnt waits retire these stores before any record is written)
-  if (a.partial) {
-    for (int c = tid; c < a.Ncols * HALO_WMW; c += NT) {
-      float* rec = a.partial + ((long)(c / HALO_WMW) * G * HALO_WMW + (long)g * HALO_WMW + c % HALO_WMW) * 3;
-      rec[0] = rec[1] = rec[2] = 0.f;
-    }
-  }
-  if (u0 >= u1) return;
-
-  // a tile: column block cb, output pixels [m0, m0 + rows)
-  auto tile_rows = [&](long u, int& cb, int& m0) {
-    cb = (int)(u / M);
-    m0 = (int)(u - (long)cb * M);
-    const long end = min(u1, (long)(cb + 1) * M);
-    return (int)min((long)a.tm, end - u);
-  };
-  // always NXW instructions per wave (pixels past the window read zeros), so
-  // the counted vmcnt waits below see a fixed number of younger operations
-  auto issue_x = [&](int pr_lo, int npx, int cc, char* Xs) {
-#pragma unroll 1
-    for (int k = 0; k < NXW; ++k) {
-      const int i = wave + NWI * k;
-      const int px = i * 8 + (lane >> 3);
-      const int pr = pr_lo + (px >> a.lxw), pc = px & (XW - 1);
-      const int n = (int)fdiv((uint32_t)pr, a.div_hp), ip = pr - n * Hp - 1, iw = pc - 1;
-      const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
-      const bool ok = px < npx && (uint32_t)ip < (uint32_t)a.H && (uint32_t)iw < (uint32_t)a.W;
-      const uint32_t off = (uint32_t)(((((long)n * a.H + ip) * a.W + iw) * a.Cr + cc * 64 + ch * 8) * 2);
-      blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
-    }
-  };
-  // weight rows of the column block: per lane its rows' byte offsets at tap 0, chunk 0
-  uint32_t woff[LB];
-  auto set_woff = [&](int cb) {
-#pragma unroll
-    for (int l = 0; l < LB; ++l) {
-      const int row = 8 * (wave + NWI * l) + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);  // ktile_off's swizzle
-      woff[l] = (uint32_t)((((long)cb * BN + row) * 9 * a.Cr + c * 8) * 2);
-    }
-  };
-  auto issue_b = [&](int cc, int t, char* Bs) {
-    const uint32_t k = (uint32_t)((t * a.Cr + cc * 64) * 2);
-#pragma unroll
-    for (int l = 0; l < LB; ++l) blds16(rsW, woff[l] + k, Bs + (wave + NWI * l) * 1024);
-  };
-
-  int boff[FN][2];
-#pragma unroll
-  for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) boff[jj][kh] = ktile_off(wn * WTN + jj * 16 + (lane & 15), 4 * kh + kq);
-  const int rbase = wm * WTM + kq * 4, cbase = wn * WTN + (lane & 15);
-
-  WaveStats<FM, FN> ws;
-  ws.reset();
-
-  long u = u0;
-  int cb, m0;
-  int rows = tile_rows(u, cb, m0);
-  int pr_lo, npx;
-  hb_window(a, m0, rows, pr_lo, npx);
-  char* const Xbuf = smem + NSB * B_BYTES;
-  const bool g1 = wave >= 4;  // group 1: waves 4-7, one beside each group-0 wave on its SIMD
-  set_woff(cb);
-  issue_x(pr_lo, npx, 0, Xbuf);
-  issue_b(0, 0, smem);
-  issue_b(0, 1, smem + B_BYTES);
-  int xb = 0, sb = 0;  // window buffer of the current chunk, weight stage of the current k-step
-  for (;;) {
-    // this tile's A-fragment LDS addresses for each column shift s of a tap
-    // (the row shift r XW * 128 B is added per k-step)
-    // (k-half 1's slot is k-half 0's with bit 2 flipped: address ^ 64, which
-    // commutes with the row shift, a multiple of 2 KiB)
-    int abase[FM][3];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int r = wm * WTM + i * 16 + (lane & 15);
-      const int m = m0 + min(r, rows - 1);
-      const int n = m / HW, rem = m - n * HW, p = rem / a.W, q = rem - p * a.W;
-      const int pxb = ((n * Hp + p - pr_lo) << a.lxw) + q;
-#pragma unroll
-      for (int s3 = 0; s3 < 3; ++s3) abase[i][s3] = xtile_off(pxb + s3, kq);
-    }
-    const bool wact = wm * WTM < rows;  // the wave has rows in this tile (uniform)
-    // the next tile (its window is issued during this tile's last chunk)
-    const long un = u + rows;
-    const bool more = un < u1;
-    int cbn = cb, m0n = m0, rowsn = 0, pr_lon = 0, npxn = 0;
-    if (more) {
-      rowsn = tile_rows(un, cbn, m0n);
-      hb_window(a, m0n, rowsn, pr_lon, npxn);
-    }
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // The tile's k-loop as a two-group ping-pong (MI355X_MICROARCH.md, "Two
-    // waves per SIMD"): every wave runs read(s) | mfma(s) | read(s+1) | ...
-    // with a barrier at each "|", and group 1 (waves 4-7) passes one extra
-    // barrier first, so on every SIMD one wave multiplies while its partner
-    // reads fragments and issues its share of the LDS-DMA (weights of k-step
-    // s + 2; at a chunk's second k-step the next chunk's window).  After its
-    // reads a wave retires them (lgkmcnt(0): the stage they read may be
-    // refilled after the next barrier) and, with a counted vmcnt, its share
-    // of k-step s + 1's weights (read after the barrier after next).
-    // NF = this wave's valid row fragments (uniform): fragments past the
-    // tile's rows are neither read nor multiplied.
-    auto kloop = [&](auto nfc) {
-      constexpr int NF = decltype(nfc)::value;
-      bool switched = false;  // woff moved on to the next tile's column block
-      auto bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      // everything this tile's first k-step reads has landed (and the previous
-      // tile's epilogue stores have retired)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (g1) bar();
-      for (int cc = 0; cc < nc; ++cc) {
-        char* const Xs = Xbuf + xb * HB_XBUF;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          char* const Bs = smem + sb * B_BYTES;
-          // ---- read(s) + this wave's DMA share
-          bar();
-          Frag<T> fa[2][FM], fb[2][FN];
-          if (NF > 0 && a.dbg != 1) {
-            // DGRAD: weight tap t reads dy at the flipped shift 8 - t
-            const int tt = FLIP ? 8 - t : t;
-            const int rr = tt / 3, s3 = tt % 3;
-            const int roff = (rr << a.lxw) * 128;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-#pragma unroll
-              for (int i = 0; i < NF; ++i)
-                fa[h][i].v = *reinterpret_cast<const bf16x8*>(Xs + ((abase[i][s3] + roff) ^ (h << 6)));
-#pragma unroll
-              for (int jj = 0; jj < FN; ++jj) fb[h][jj].v = *reinterpret_cast<const bf16x8*>(Bs + boff[jj][h]);
-            }
-          }
-          {
-            // weights of k-step s + 2 into the stage k-step s - 1 was read from
-            const int sb2 = sb == 0 ? 2 : sb - 1;
-            const int t2 = t + 2 < 9 ? t + 2 : t - 7;
-            int cc2 = t + 2 < 9 ? cc : cc + 1;
-            if (cc2 >= nc) {  // the next tile's k-steps (or, with none left, a dummy that keeps the count)
-              if (more && !switched && cbn != cb) set_woff(cbn);
-              switched = true;
-              cc2 = 0;
-            }
-            issue_b(cc2, more || cc2 > 0 || t + 2 < 9 ? t2 : 0, smem + sb2 * B_BYTES);
-            // the next chunk's window into the buffer the previous chunk was
-            // read from (both groups finished it before this k-step)
-            if (t == 1) {
-              const bool same = cc + 1 < nc;
-              issue_x(same ? pr_lo : pr_lon, same ? npx : (more ? npxn : 0), same ? cc + 1 : 0,
-                      Xbuf + (xb ^ 1) * HB_XBUF);
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          // younger than k-step s + 1's weights: k-step s + 2's and the window
-          // instructions of k-steps with t == 1 (this one or the previous one)
-          if (t == 1 || t == 2) asm volatile("s_waitcnt lgkmcnt(0) vmcnt(%0)" ::"n"(LB + NXW) : "memory");
-          else asm volatile("s_waitcnt lgkmcnt(0) vmcnt(%0)" ::"n"(LB) : "memory");
-          // ---- mfma(s)
-          bar();
-          if (NF > 0 && a.dbg != 1) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-              for (int i = 0; i < NF; ++i)
-#pragma unroll
-                for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[h][i], fb[h][jj]);
-          }
-          sb = sb == NSB - 1 ? 0 : sb + 1;
-        }
-        xb ^= 1;
-      }
-      if (!g1) bar();
-    };
-    const int nf = wact ? (a.dbg == 2 ? FM : min(FM, (rows - wm * WTM + 15) >> 4)) : 0;
-    static_assert(FM == 4, "kloop dispatch");
-    if (nf == 4) kloop(std::integral_constant<int, 4>());
-    else if (nf == 3) kloop(std::integral_constant<int, 3>());
-    else if (nf == 2) kloop(std::integral_constant<int, 2>());
-    else if (nf == 1) kloop(std::integral_constant<int, 1>());
-    else kloop(std::integral_constant<int, 0>());
-
-    // ---- epilogue: 16-bit stores from the accumulators
-    uint32_t rowoff[FM][4];
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = rbase + i * 16 + e;
-        const bool v = r < rows;
-        rowoff[i][e] = v ? (uint32_t)((((long)(m0 + r)) * a.Ncols + cb * BN + cbase) * 2) : 0x80000000u;
-        vmask |= (v ? 1u : 0u) << (i * 4 + e);
-      }
-    if (a.partial && wact) ws.tile(acc, vmask);
-    if (a.add) {
-      short r[FM][FN][4];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) r[i][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsA, rowoff[i][e] + jj * 32, 0, 0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = to_f32(from_f32<T>(acc[i][jj][e])) + to_f32(__builtin_bit_cast(T, r[i][jj][e]));
-            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(v)), rsO,
-                                                  rowoff[i][e] + jj * 32, 0, 0);
-          }
-    } else {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, from_f32<T>(acc[i][jj][e])), rsO,
-                                                  rowoff[i][e] + jj * 32, 0, 0);
-    }
-    // BN records of the column block when it ends (range end or block change)
-    if (a.partial && (!more || cbn != cb)) {
-      float n, mean[FN], m2[FN];
-      ws.wave_merge(n, mean, m2);
-      if (lane < 16) {
-#pragma unroll
-        for (int jj = 0; jj < FN; ++jj) {
-          const int c = cb * BN + cbase + jj * 16;
-          float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
-          rec[0] = n;
-          rec[1] = mean[jj] * n;
-          rec[2] = m2[jj];
-        }
-      }
-      ws.reset();
-    }
-    if (!more) break;
-    u = un; cb = cbn; m0 = m0n; rows = rowsn; pr_lo = pr_lon; npx = npxn;
-  }
-  // the dummy prefetches land before the workgroup's LDS is released
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -2981,239 +2326,15 @@ struct StemBwArgs {
   float* slab;          // [G][64][224]
   uint32_t x_bytes, y_bytes, dp_bytes, ix_bytes;
   int N, H, W, P, Q, P2, Q2, tiles;
-  int diag;  // SSIP_STEM_DIAG (timing experiments only): 1 = skip the dy pass, 2 = skip the MFMAs, 8 = per-pixel gather
 };
 
 constexpr int SBW_Y = 28 * 1024, SBW_DP = 14 * 1024, SBW_IX = 7 * 1024;
 constexpr int SBW_IN = STEM_XBUF + SBW_Y + SBW_DP + SBW_IX;  // one input buffer (66 KiB)
-constexpr int SBW_D = 28 * 1024;                             // dy image: 224 rows x 128 B
 
-__global__ void __launch_bounds__(512, 2) conv_stem_bwd_wgrad_kernel(const StemBwArgs a) {
-  typedef __bf16 T;
-  typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
-  constexpr int NW = 8, NB = 14, MR = 224;  // column blocks; GEMM rows (2 x 112 output pixels)
-  static_assert(2 * SBW_IN + SBW_D <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * SBW_IN + SBW_D];
-  char* const Dimg = smem + 2 * SBW_IN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int G = gridDim.x, g = blockIdx.x;
-  const int u0 = (int)((long)g * a.tiles / G), u1 = (int)((long)(g + 1) * a.tiles / G);
-  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsY = make_rsrc(a.Y, a.y_bytes);
-  const __amdgpu_buffer_rsrc_t rsP = make_rsrc(a.DP, a.dp_bytes), rsI = make_rsrc(a.IX, a.ix_bytes);
-  const int xpitch = a.W * 8;
-  const int xrun = STEM_XROWS * xpitch;
-  const int yrun = 2 * a.Q * 128, prow = a.Q2 * 128, irow = a.Q2 * 64;
-
-  auto issue = [&](int tile, char* B) {
-    const int R0 = tile * 2;  // conv-output rows R0, R0+1 of the flattened (n, p) space
-    const int n = R0 / a.P, h0 = R0 - n * a.P, T0 = h0 >> 1;
-    const uint32_t xb = (uint32_t)((((long)n * a.H + 2 * h0) * a.W) * 8);  // input rows 2 h0 .. 2 h0 + 8
-    const uint32_t yb = (uint32_t)((((long)n * a.P + h0) * a.Q) * 128);
-    const int prows = (T0 + 1 < a.P2) ? 2 : 1;
-    const uint32_t pb = (uint32_t)((((long)n * a.P2 + T0) * a.Q2) * 128);
-    const uint32_t ib = (uint32_t)((((long)n * a.P2 + T0) * a.Q2) * 64);
-    for (int i = wave; i < STEM_XBUF / 1024; i += NW) {
-      const int b = i * 1024 + lane * 16;
-      blds16(rsX, b < xrun ? xb + (uint32_t)b : SSIP_OOB, B + i * 1024);
-    }
-    for (int i = wave; i < SBW_Y / 1024; i += NW) {
-      const int b = i * 1024 + lane * 16;
-      blds16(rsY, b < yrun ? yb + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + i * 1024);
-    }
-    for (int i = wave; i < SBW_DP / 1024; i += NW) {
-      const int b = i * 1024 + lane * 16;
-      blds16(rsP, b < prows * prow ? pb + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + SBW_Y + i * 1024);
-    }
-    for (int i = wave; i < SBW_IX / 1024; i += NW) {
-      const int b = i * 1024 + lane * 16;
-      blds16(rsI, b < prows * irow ? ib + (uint32_t)b : SSIP_OOB, B + STEM_XBUF + SBW_Y + SBW_DP + i * 1024);
-    }
-  };
-
-  // this thread's 8-channel chunk in the dy pass is fixed (items id = tid + 512 i)
-  const int cc = tid & 7, c0 = cc * 8;
-  float sc[8], sh[8], ca[8], cb[8], ck[8];
-  load_f8(sc, a.scale + c0);
-  load_f8(sh, a.shift + c0);
-  load_f8(ca, a.coef + c0);
-  load_f8(cb, a.coef + 64 + c0);
-  load_f8(ck, a.coef + 128 + c0);
-
-  const int nbw = wn < NB - 12 ? 4 : 3;
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[x][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int lg = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
-
-  if (u0 < u1) issue(u0, smem);
-  bool first = true;
-  for (int u = u0; u < u1; ++u) {
-    char* const Bc = smem + ((u - u0) & 1) * SBW_IN;
-    char* const Bn = smem + ((u - u0 + 1) & 1) * SBW_IN;
-    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    first = false;
-    halo_lds_barrier();  // this tile's inputs landed; the dy image and the other buffer are free
-    if (u + 1 < u1) issue(u + 1, Bn);
-    if (!(a.diag & 1)) {
-      // ---- dy for the tile's 224 output pixels, into the m-major MTile image
-      const int R0 = u * 2;
-      const int h0 = R0 - (R0 / a.P) * a.P, T0 = h0 >> 1;
-      const char* Ys = Bc + STEM_XBUF;
-      const char* Ps = Ys + SBW_Y;
-      const char* Is = Ps + SBW_DP;
-      if (!(a.diag & 8)) {
-        // 2x2 pixel blocks: rows (h0, h0+1) x columns (2l, 2l+1), one 8-channel
-        // chunk per thread.  h0 is even, so row h0 lies only in pooled row T0
-        // (window row 1), row h0+1 in T0 (row 2) and T0+1 (row 0); likewise
-        // column 2l in window l (column 1), 2l+1 in l (2) and l+1 (0).  The
-        // block's four windows are read once and every (window, pixel) pair
-        // is tested without branches; contributions are added in the same
-        // (p, q)-ascending order as the per-pixel gather below.
-        const int QH = a.Q >> 1;
-        if (tid < QH * 8) {
-          const int l = tid >> 3;
-          const bool q1 = l + 1 < a.Q2, p1 = T0 + 1 < a.P2;
-          const uint64_t NOHIT = ~0ull;  // no argmax byte is 255
-          uint64_t k00, k01 = NOHIT, k10 = NOHIT, k11 = NOHIT;
-          Vec8<T> g00, g01, g10, g11;
-          k00 = *reinterpret_cast<const uint64_t*>(Is + l * 64 + c0);
-          g00.v = *reinterpret_cast<const i32x4*>(Ps + l * 128 + c0 * 2);
-          g01.v = g10.v = g11.v = (i32x4){0, 0, 0, 0};
-          if (q1) {
-            k01 = *reinterpret_cast<const uint64_t*>(Is + (l + 1) * 64 + c0);
-            g01.v = *reinterpret_cast<const i32x4*>(Ps + (l + 1) * 128 + c0 * 2);
-          }
-          if (p1) {
-            k10 = *reinterpret_cast<const uint64_t*>(Is + (a.Q2 + l) * 64 + c0);
-            g10.v = *reinterpret_cast<const i32x4*>(Ps + (a.Q2 + l) * 128 + c0 * 2);
-            if (q1) {
-              k11 = *reinterpret_cast<const uint64_t*>(Is + (a.Q2 + l + 1) * 64 + c0);
-              g11.v = *reinterpret_cast<const i32x4*>(Ps + (a.Q2 + l + 1) * 128 + c0 * 2);
-            }
-          }
-          float dz[4][8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int b00 = (int)((k00 >> (8 * e)) & 0xff), b01 = (int)((k01 >> (8 * e)) & 0xff);
-            const int b10 = (int)((k10 >> (8 * e)) & 0xff), b11 = (int)((k11 >> (8 * e)) & 0xff);
-            const float v00 = g00.get(e), v01 = g01.get(e), v10 = g10.get(e), v11 = g11.get(e);
-            float d;
-            d = 0.f; if (b00 == 4) d += v00;
-            dz[0][e] = d;
-            d = 0.f; if (b00 == 5) d += v00; if (b01 == 3) d += v01;
-            dz[1][e] = d;
-            d = 0.f; if (b00 == 7) d += v00; if (b10 == 1) d += v10;
-            dz[2][e] = d;
-            d = 0.f; if (b00 == 8) d += v00; if (b01 == 6) d += v01; if (b10 == 2) d += v10; if (b11 == 0) d += v11;
-            dz[3][e] = d;
-          }
-#pragma unroll
-          for (int px = 0; px < 4; ++px) {
-            const int m = (px >> 1) * a.Q + 2 * l + (px & 1);
-            Vec8<T> yy, o;
-            yy.v = *reinterpret_cast<const i32x4*>(Ys + m * 128 + c0 * 2);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float yv = yy.get(e);
-              const float t = __builtin_fmaf(yv, sc[e], sh[e]);
-              const float d = (t > 0.f ? t : 0.f) > 0.f ? dz[px][e] : 0.f;
-              o.set(e, ca[e] * d + cb[e] * yv + ck[e]);
-            }
-            *reinterpret_cast<i32x4*>(Dimg + m * 128 + ((cc ^ ((m & 3) << 1)) << 4)) = o.v;
-          }
-        }
-      } else
-      for (int id = tid; id < MR * 8; id += 512) {
-        const int m = id >> 3;
-        const int j = m >= a.Q ? 1 : 0, w = m - j * a.Q, h = h0 + j;
-        // windows (p, q) with 2p-1 <= h <= 2p+1, 2q-1 <= w <= 2q+1 (k 3, s 2, pad 1), p, q ascending
-        float dz[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dz[e] = 0.f;
-        const int plo = h >> 1, phi = min((h + 1) >> 1, a.P2 - 1);
-        const int qlo = w >> 1, qhi = min((w + 1) >> 1, a.Q2 - 1);
-#pragma unroll
-        for (int pa = 0; pa < 2; ++pa) {
-          const int pp = plo + pa;
-          if (pp > phi) continue;
-          const int pr = pp - T0;  // 0 or 1: the staged pooled row
-#pragma unroll
-          for (int qb = 0; qb < 2; ++qb) {
-            const int qq = qlo + qb;
-            if (qq > qhi) continue;
-            const int pos = (h - (2 * pp - 1)) * 3 + (w - (2 * qq - 1));
-            const uint64_t pk = *reinterpret_cast<const uint64_t*>(Is + (pr * a.Q2 + qq) * 64 + c0);
-            Vec8<T> gv;
-            gv.v = *reinterpret_cast<const i32x4*>(Ps + (pr * a.Q2 + qq) * 128 + c0 * 2);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if ((int)((pk >> (8 * e)) & 0xff) == pos) dz[e] += gv.get(e);
-          }
-        }
-        Vec8<T> yy, o;
-        yy.v = *reinterpret_cast<const i32x4*>(Ys + (j * a.Q + w) * 128 + c0 * 2);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float yv = yy.get(e);
-          const float t = __builtin_fmaf(yv, sc[e], sh[e]);
-          const float d = (t > 0.f ? t : 0.f) > 0.f ? dz[e] : 0.f;
-          o.set(e, ca[e] * d + cb[e] * yv + ck[e]);
-        }
-        *reinterpret_cast<i32x4*>(Dimg + m * 128 + ((cc ^ ((m & 3) << 1)) << 4)) = o.v;
-      }
-    }
-    halo_lds_barrier();  // dy image complete
-    const char* Xs = Bc;
-#pragma unroll
-    for (int ks = 0; ks < ((a.diag & 2) ? 0 : MR / 32); ++ks) {
-      Frag<T> fa[2], fb[4];
-#pragma unroll
-      for (int x = 0; x < 2; ++x) read_tfrag(fa[x], Dimg, 32 * ks, (2 * wm + x) * 16, lane);
-      const int m_lo = 32 * ks + 8 * lg + lq, m_hi = m_lo + 4;
-      const int jl = m_lo >= a.Q ? 1 : 0, ql = m_lo - jl * a.Q;
-      const int jh = m_hi >= a.Q ? 1 : 0, qh = m_hi - jh * a.Q;
-      const int base_lo = 2 * jl * xpitch + ql * 16, base_hi = 2 * jh * xpitch + qh * 16;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        if (b < nbw) {
-          const int nb = wn + 4 * b, r = nb >> 1, cofs = ((nb & 1) * 16 + 4 * lp) * 2;
-          const char* a0 = Xs + base_lo + r * xpitch + cofs;
-          const char* a1 = Xs + base_hi + r * xpitch + cofs;
-          v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a0));
-          v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a1));
-          fb[b].v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-      }
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if (b < nbw) mma(acc[x][b], fa[x], fb[b]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  float* sl = a.slab + (long)g * 64 * 224;
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (b < nbw)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = (2 * wm + x) * 16 + 4 * (lane >> 4) + e;
-          const int col = (wn + 4 * b) * 16 + (lane & 15);
-          sl[(long)k * 224 + col] = acc[x][b][e];
-        }
-}
-
-// The same fused stem backward tail with the two halves specialised
-// (tools/time_stem_bw.py: DMA + sync alone 133 us, the dy pass +72, the
-// MFMAs +74, and the two do not overlap in conv_stem_bwd_wgrad_kernel, where
-// every wave runs both behind a barrier): waves 0-7 form dy (two per SIMD,
+// The two halves of the work are specialised (tools/time_stem_bw.py on
+// round 2's form, where every wave ran both behind a barrier -- r3-variants
+// branch: DMA + sync alone 133 us, the dy pass +72, the MFMAs +74, and the
+// two did not overlap): waves 0-7 form dy (two per SIMD,
 // 4 channels x one 2x2 block per thread), waves 8-11 multiply (one per SIMD,
 // all 64 k x 3-4 column blocks).  A tile's 224 GEMM rows are cut into half A (output columns
 // 0-63 of both rows: 128 rows, 4 k-steps) and half B (columns 64-111: 96
@@ -3315,7 +2436,6 @@ __global__ void __launch_bounds__(768, 1) conv_stem_bwd_wgrad2_kernel(const Stem
   // half h of tile `tile` into slot D (GEMM row of pixel (j, q) = chunk * 32 + j * 16 + q % 16,
   // chunk = (q - q0) / 16 with q0 the half's first column)
   auto produce = [&](int tile, int h, char* D) {
-    if (a.diag & 1) return;
     const int nblk = h == 0 ? 32 : 24;
     if (lb >= nblk) return;
     const int R0 = tile * 2;
@@ -3385,7 +2505,6 @@ __global__ void __launch_bounds__(768, 1) conv_stem_bwd_wgrad2_kernel(const Stem
   const int nbw = mw < NB - 12 ? 4 : 3;
   const int lg = lane >> 4, lq = (lane & 15) >> 2, lp = lane & 3;
   auto consume = [&](f32x4 (&acc)[4][4], int tile, int h, const char* D) {
-    if (a.diag & 2) return;
     const char* Xs = buf(tile);
     const int nks = h == 0 ? 4 : 3, q0 = h == 0 ? 0 : 64;
     for (int ks = 0; ks < nks; ++ks) {
@@ -3632,7 +2751,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
       splits = std::min(max_splits, ceil_div(std::max(1, atoi(e)), tiles));
     } else if (pl.stages > 0) {
       const int nt = 64 * pl.wmw * pl.wnw;
-      const int nbuf = (pl.stages == 5 || pl.stages == 8) ? 2 : std::max(2, pl.stages);
+      const int nbuf = std::max(2, pl.stages);
       const int lds = nbuf * 64 * (pl.bm + pl.bn) * 2;
       const int per_cu = std::max(1, std::min(2048 / nt, 163840 / lds));
       const long slots = (long)device_cus() * per_cu;
@@ -3660,26 +2779,14 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   return SSIP_OK;
 }
 
-// LDS-DMA ring kernel configurations (bm, bn, waves_m, waves_n, stages).
-#define SSIP_GLDS_FD(X)                                                                                      \
-  X(256, 128, 4, 2, 3) X(256, 128, 4, 2, 2) X(256, 64, 4, 1, 2) X(256, 64, 4, 1, 3) X(256, 64, 4, 2, 2)        \
-  X(256, 64, 4, 2, 3) X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 2, 3)      \
-  X(128, 64, 2, 2, 2) X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(128, 64, 4, 2, 2) X(128, 128, 4, 4, 2)      \
-  X(256, 128, 4, 4, 2) X(128, 64, 4, 2, 3) X(128, 128, 4, 4, 3) X(256, 128, 4, 4, 3)             \
-  X(256, 128, 2, 2, 2) X(512, 64, 4, 1, 2) X(256, 256, 2, 2, 2) X(256, 256, 4, 2, 2) X(512, 64, 8, 1, 2)      \
-  X(256, 128, 4, 2, 5) X(512, 64, 8, 1, 5) X(128, 128, 4, 2, 5) X(256, 64, 8, 1, 5) X(256, 256, 2, 4, 8)
-#define SSIP_GLDS_WG(X)                                                                                      \
-  X(128, 128, 2, 2, 2) X(128, 128, 2, 2, 3) X(128, 128, 2, 4, 2) X(128, 128, 2, 4, 3) X(128, 64, 2, 2, 2)      \
-  X(128, 64, 2, 2, 3) X(128, 64, 2, 1, 2) X(64, 128, 1, 4, 2) X(64, 128, 1, 4, 3) X(64, 128, 1, 2, 2)          \
-  X(64, 128, 1, 8, 3) X(128, 128, 4, 2, 2) X(128, 128, 4, 4, 2) X(128, 64, 2, 4, 2) X(64, 128, 2, 4, 2)      \
-  X(64, 128, 1, 8, 2) X(128, 128, 4, 4, 3) X(64, 128, 2, 4, 3) X(128, 64, 2, 4, 3) X(256, 128, 4, 4, 2)    \
-  X(128, 256, 2, 2, 2) X(256, 128, 2, 2, 2) X(64, 256, 1, 2, 2) X(256, 256, 2, 2, 2) X(128, 128, 2, 4, 5)    \
-  X(128, 128, 4, 2, 5) X(256, 128, 4, 2, 5) X(128, 256, 2, 4, 5) X(64, 128, 2, 4, 5) X(64, 256, 1, 8, 5) \
-  X(256, 256, 2, 4, 8)
-
+// LDS-DMA ring kernel configurations (bm, bn, waves_m, waves_n, stages):
+// the ones choose_glds() selects (round 3's wider tuning sets are on the
+// r3-variants branch, with tools/tune_conv.py's lists)
+#define SSIP_GLDS_FD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2) X(128, 128, 4, 4, 3)
+#define SSIP_GLDS_WG(X) X(128, 128, 4, 2, 2) X(64, 128, 2, 4, 2)
 #define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
-#define SSIP_GLDS_FOLD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2) X(128, 128, 4, 4, 3)
-#define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2) X(256, 64, 4, 2, 2) X(128, 64, 2, 2, 2) X(256, 64, 4, 1, 2)
+#define SSIP_GLDS_FOLD(X) SSIP_GLDS_FD(X)
+#define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2)
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st) {
 #define SSIP_GLDS_EQ(BM_, BN_, WM_, WN_, ST_) \
@@ -3697,39 +2804,11 @@ static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st
 
 template <int MODE>
 static int launch_glds(const Plan& pl, hipStream_t st) {
-  SSIP_REQUIRE(pl.stages != 8 || !pl.args.phased, SSIP_ERR_ARG,
-               "the 8-phase kernel has no stride-2 dgrad phase split");
-  SSIP_REQUIRE(pl.stages != 8 || MODE != MODE_WGRAD || (pl.args.C % 256 == 0 && pl.args.K % 256 == 0), SSIP_ERR_ARG,
-               "the 8-phase wgrad needs C and K multiples of 256 (one tap per 256-column tile)");
-  // SSIP_WG_LDSPAD (tuning): extra LDS bytes per wgrad workgroup, to cap how
-  // many share a CU with the main stream's kernels
-  static const int wg_ldspad = getenv("SSIP_WG_LDSPAD") ? atoi(getenv("SSIP_WG_LDSPAD")) : 0;
-  const unsigned dyn_lds = MODE == MODE_WGRAD ? (unsigned)wg_ldspad : 0u;
 #define SSIP_GLDS_GO(BM_, BN_, WM_, WN_, ST_)                                                                 \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_),      \
-                       dyn_lds, st, pl.args);                                                                 \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
+                       st, pl.args);                                                                          \
     return ::ssip::check_launch("conv_glds");                                                                 \
-  }
-  {
-    // SSIP_LOOP_DIAG (timing experiments only): conv_glds_kernel's LDIAG ablations
-    static const int ldiag = getenv("SSIP_LOOP_DIAG") ? atoi(getenv("SSIP_LOOP_DIAG")) : 0;
-    if (ldiag && pl.args.pmean == nullptr && pl.args.bias == nullptr && !pl.conv1 && pl.stages == 2 &&
-        pl.wmw == 4 && pl.wnw == 2 && ((pl.bm == 128 && pl.bn == 128) || (pl.bm == 256 && pl.bn == 256))) {
-#define SSIP_GLDS_GOD(D_)                                                                                     \
-  if (ldiag == D_) {                                                                                          \
-    if (pl.bm == 128)                                                                                         \
-      hipLaunchKernelGGL((conv_glds_kernel<MODE, 128, 128, 4, 2, 2, false, false, false, D_>), pl.grid,      \
-                         dim3(512), 0, st, pl.args);                                                          \
-    else                                                                                                      \
-      hipLaunchKernelGGL((conv_glds_kernel<MODE, 256, 256, 4, 2, 2, false, false, false, D_>), pl.grid,      \
-                         dim3(512), 0, st, pl.args);                                                          \
-    return ::ssip::check_launch("conv_glds_diag");                                                            \
-  }
-      SSIP_GLDS_GOD(1) SSIP_GLDS_GOD(2) SSIP_GLDS_GOD(3) SSIP_GLDS_GOD(4) SSIP_GLDS_GOD(5) SSIP_GLDS_GOD(6)
-      SSIP_GLDS_GOD(8) SSIP_GLDS_GOD(12)
-#undef SSIP_GLDS_GOD
-    }
   }
   if constexpr (MODE == MODE_WGRAD) {
     SSIP_GLDS_WG(SSIP_GLDS_GO)
@@ -3784,18 +2863,7 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
 template <int MODE, typename T>
 static int launch_conv(const Plan& pl, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
-    if (pl.stages > 0) {
-      // SSIP_DIAG (timing experiments only): 1 = drop the A operand's loads,
-      // 2 = drop B's (zero-extent buffer resources read zeros; results are wrong)
-      static const int diag = getenv("SSIP_DIAG") ? atoi(getenv("SSIP_DIAG")) : 0;
-      if (diag) {
-        Plan p2 = pl;
-        if (diag & 1) p2.args.a_bytes = 0;
-        if (diag & 2) p2.args.b_bytes = 0;
-        return launch_glds<MODE>(p2, st);
-      }
-      return launch_glds<MODE>(pl, st);
-    }
+    if (pl.stages > 0) return launch_glds<MODE>(pl, st);
   }
 #define SSIP_LAUNCH(BM_, BN_, WM_, WN_, C1_)                                                                  \
   {                                                                                                           \
@@ -3941,10 +3009,8 @@ static bool halo_plan(int mode, const ssip_conv_desc* d, int dtype, HaloPlan& hp
   hp.cols = cols;
   hp.tiles = (int)((long)d->N * d->H / TR);
   hp.units = hp.tiles * (cols / 64);
-  // persistent: one workgroup per CU (SSIP_HALO_GMUL: that many per CU, each
-  // over fewer tiles -- a tuning override)
-  static const int gmul = getenv("SSIP_HALO_GMUL") ? std::max(1, atoi(getenv("SSIP_HALO_GMUL"))) : 1;
-  hp.G = std::min(hp.units, gmul * device_cus());
+  // persistent: one workgroup per CU
+  hp.G = std::min(hp.units, device_cus());
   return true;
 }
 
@@ -4053,169 +3119,18 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   h.N = d->N; h.H = d->H; h.W = d->W; h.Ncols = hp.cols;
   h.TR = hp.TR; h.tiles = hp.tiles; h.units = hp.units;
   h.flip = mode == MODE_DGRAD ? 1 : 0;
-  { const char* dbg = getenv("SSIP_HALO_DBG"); h.dbg = dbg ? atoi(dbg) : 0; }
-  // 8 waves of 64x32 by default.  SSIP_HALO_WAVES=16 (16 waves of 32x32, 4 per
-  // SIMD, VGPR-capped: spills) is ~10 % faster in isolation but 3 % slower in
-  // the step, where the side streams' kernels run beside it; 4 = 64x64 waves
-  const char* e = getenv("SSIP_HALO_WAVES");
-  int nw = 8;
-  if (e && e[0]) {
-    char* end = nullptr;
-    nw = (int)strtol(e, &end, 10);
-    if (*end || (nw != 4 && nw != 8 && nw != 16)) {
-      ::ssip::set_error("SSIP_HALO_WAVES=\"%s\": must be 4, 8 or 16", e);
-      return SSIP_ERR_ARG;
-    }
-  }
+  // 8 waves of 64x32 (16 waves of 32x32 were ~10 % faster in isolation but 3 %
+  // slower in the step, where the side streams' kernels run beside them; 4
+  // waves of 64x64 slower still: r3-variants branch)
   if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bp != nullptr)
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bias != nullptr)  // folded eval BN epilogue
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
-  else if (nw == 4)
-    hipLaunchKernelGGL((conv_halo_kernel<4, 1>), dim3(hp.G), dim3(256), 0, st, h);
-  else if (nw == 8)
+  else
     hipLaunchKernelGGL((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
-  else
-    hipLaunchKernelGGL((conv_halo_kernel<8, 2>), dim3(hp.G), dim3(1024), 0, st, h);
   return ::ssip::check_launch("conv_halo");
-}
-
-// ---- row-balanced halo path (conv_hb_kernel): 3x3 / stride 1 / pad 1, bf16,
-// >= 128 reduction channels (multiple of 64), output channels a multiple of
-// the column block.  SSIP_HB=0 turns it off; an SSIP_CONV_FORCE for the pass
-// selects the implicit-GEMM kernels instead.
-struct HbPlan {
-  int BN, G, cols, redc, lxw, tm;
-  long units;
-};
-
-static bool hb_plan_compute(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp);
-
-// hb_plan_compute's tile search walks every workgroup's tiles: cached per
-// geometry (per thread), so a launch costs the host a lookup
-static bool hb_plan(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
-  // Off by default: faster per launch where it applies (l2 / l3 3x3 at batch
-  // 256: -4..-10 %, tools/time_hb.py) but slower in the train step (6.59 vs
-  // 6.49 ms/step: a persistent workgroup holding a CU's whole LDS keeps the
-  // side streams' kernels off it; profiles/r3_hb.txt).  SSIP_HB=1: wherever
-  // the kernel applies; =2: where it measured faster per launch (LDS rows at
-  // least 3/4 filled -- W + 2 >= 3/4 of the power-of-two pitch -- and full
-  // 256-pixel tiles); =f / =d / =n: that rule for the forward / the dgrad /
-  // batches of 256+ only.
-  const char* e = getenv("SSIP_HB");
-  if (!e || !e[0] || e[0] == '0') return false;
-  const int force = e[0] == '1' ? 1 : -1;
-  if (e && ((e[0] == 'f' && mode != MODE_FWD) || (e[0] == 'd' && mode != MODE_DGRAD))) return false;
-  if (e && e[0] == 'n' && d->N < 256) return false;  // =n: batches of 256+ only (the train pass, not the weak forward)
-  const char* f = getenv("SSIP_CONV_FORCE");
-  if (f && f[0] == (mode == MODE_FWD ? 'f' : 'd')) return false;
-  struct Entry {
-    int key[12];
-    bool ok;
-    HbPlan hp;
-  };
-  static thread_local Entry cache[32];
-  static thread_local int ncache = 0, next = 0;
-  const int key[12] = {mode, dtype, d->N, d->H, d->W, d->C, d->K, d->R, d->S, d->stride, d->pad, device_cus()};
-  const Entry* hit = nullptr;
-  for (int i = 0; i < ncache && !hit; ++i)
-    if (memcmp(cache[i].key, key, sizeof(key)) == 0) hit = &cache[i];
-  if (!hit) {
-    Entry& en = cache[next];
-    next = (next + 1) % 32;
-    ncache = std::min(ncache + 1, 32);
-    memcpy(en.key, key, sizeof(key));
-    en.ok = hb_plan_compute(mode, d, dtype, en.hp);
-    hit = &en;
-  }
-  hp = hit->hp;
-  // the same answer on every call for this geometry and environment: the
-  // BN-record sizing (ssip_conv_fwd_partial_floats / _tiles) and the launch
-  // must agree
-  if (!hit->ok) return false;
-  return force == 1 || (4 * (d->W + 2) >= 3 * (1 << hp.lxw) && hp.tm == HB_TM);
-}
-
-static bool hb_plan_compute(int mode, const ssip_conv_desc* d, int dtype, HbPlan& hp) {
-  if (dtype != SSIP_BF16 || !desc_ok(d) || d->R != 3 || d->S != 3 || d->stride != 1 || d->pad != 1 ||
-      d->P != d->H || d->Q != d->W)
-    return false;
-  const int redc = mode == MODE_FWD ? d->C : d->K;
-  const int cols = mode == MODE_FWD ? d->K : d->C;
-  const int BN = 128;
-  if (redc < 128 || redc % 64 != 0 || cols % BN != 0) return false;
-  const long M = (long)d->N * d->H * d->W;
-  if (M * redc * 2 >= (1l << 31) || M * cols * 2 >= (1l << 31) || (long)cols * 9 * redc * 2 >= (1l << 31))
-    return false;
-  hp.BN = BN;
-  hp.cols = cols;
-  hp.redc = redc;
-  hp.units = M * (cols / BN);
-  hp.G = (int)std::min<long>(device_cus(), (hp.units + 63) / 64);
-  // tile size: every tile's input window must fit one LDS buffer (hb_window);
-  // among those, the one whose slowest workgroup has the least MFMA work per
-  // SIMD (conv_hb_kernel pairs wave rows (0, 3) and (1, 2) on a SIMD and skips
-  // fragments past a tile's rows), plus one fragment's worth per tile for its
-  // prologue and epilogue
-  int lxw = 0;
-  while ((1 << lxw) < d->W + 2) ++lxw;
-  hp.lxw = lxw;
-  const int HW = d->H * d->W, Hp = d->H + 2, Wp = 1 << lxw;
-  hp.tm = 0;
-  long best = -1;
-  auto nfr = [](long rows, int wr) { return (int)std::max<long>(0, std::min<long>(4, (rows - 64 * wr + 15) / 16)); };
-  for (int tm = HB_TM; tm >= 32; tm -= 16) {
-    bool fits = true;
-    long worst = 0;
-    for (int g = 0; g < hp.G && fits; ++g) {
-      const long u0 = (long)g * hp.units / hp.G, u1 = (long)(g + 1) * hp.units / hp.G;
-      long cost = 0;
-      for (long u = u0; u < u1 && fits;) {
-        const long cb = u / M, m0 = u - cb * M;
-        const long rows = std::min<long>(tm, std::min(u1, (cb + 1) * M) - u);
-        const long m1 = m0 + rows - 1;
-        const long n0 = m0 / HW, p0 = (m0 - n0 * HW) / d->W, n1 = m1 / HW, p1 = (m1 - n1 * HW) / d->W;
-        fits = (n1 * Hp + p1 + 3 - (n0 * Hp + p0)) * Wp <= HB_XBUF / 128;
-        cost += std::max(nfr(rows, 0) + nfr(rows, 3), nfr(rows, 1) + nfr(rows, 2)) + 1;
-        u += rows;
-      }
-      worst = std::max(worst, cost);
-    }
-    if (fits && (best < 0 || worst < best)) {
-      best = worst;
-      hp.tm = tm;
-    }
-  }
-  if (hp.tm == 0) return false;
-  return true;
-}
-
-static int launch_hb(int mode, const ssip_conv_desc* d, const HbPlan& hp, const void* X, const void* Wt, void* out,
-                     const void* add, float* partial, hipStream_t st) {
-  HbArgs h;
-  memset(&h, 0, sizeof(h));
-  h.X = static_cast<const __bf16*>(X);
-  h.Wt = static_cast<const __bf16*>(Wt);
-  h.out = static_cast<__bf16*>(out);
-  h.add = static_cast<const __bf16*>(add);
-  h.partial = partial;
-  const long M = (long)d->N * d->H * d->W;
-  h.x_bytes = (uint32_t)(M * hp.redc * 2);
-  h.w_bytes = (uint32_t)((long)hp.cols * 9 * hp.redc * 2);
-  h.o_bytes = (uint32_t)(M * hp.cols * 2);
-  h.N = d->N; h.H = d->H; h.W = d->W; h.Cr = hp.redc; h.Ncols = hp.cols; h.M = (int)M;
-  h.lxw = hp.lxw;
-  h.div_hp = make_fastdiv((uint32_t)(d->H + 2));
-  h.units = hp.units;
-  h.tm = hp.tm;
-  { const char* dbg = getenv("SSIP_HB_DBG"); h.dbg = dbg ? atoi(dbg) : 0; }
-  if (mode == MODE_DGRAD)
-    hipLaunchKernelGGL((conv_hb_kernel<128, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
-  else
-    hipLaunchKernelGGL((conv_hb_kernel<128, 2, false>), dim3(hp.G), dim3(512), 0, st, h);
-  return ::ssip::check_launch("conv_hb");
 }
 
 }  // namespace
@@ -4232,8 +3147,6 @@ int64_t ssip_conv_fwd_partial_floats(const ssip_conv_desc* d) {
   HaloPlan hp;  // one record per (channel, workgroup) on the halo path
   if (halo_plan(MODE_FWD, d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
   if (stem_plan(d, SSIP_BF16, hp)) n = std::max(n, (int64_t)hp.G * HALO_WMW * d->K * 3);
-  HbPlan hb;
-  if (hb_plan(MODE_FWD, d, SSIP_BF16, hb)) n = std::max(n, (int64_t)hb.G * HALO_WMW * d->K * 3);
   // + the scratch of ssip_bn_finalize's split pass (the most records any
   // plan writes bounds the splits; the scratch starts behind the records)
   return n + fin_scratch_floats(d->K, n / (3 * d->K), 3);
@@ -4250,9 +3163,6 @@ int ssip_conv_fwd(const ssip_conv_desc* d, int dtype, const void* x, const void*
   if (halo_plan(MODE_FWD, d, dtype, hp))
     return launch_halo(MODE_FWD, d, hp, x, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream);
   if (stem_plan(d, dtype, hp)) return launch_stem_halo(d, hp, x, w_krsc, y, bn_partial, (hipStream_t)stream);
-  HbPlan hb;
-  if (hb_plan(MODE_FWD, d, dtype, hb))
-    return launch_hb(MODE_FWD, d, hb, x, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream);
   pl.args.A = x; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
@@ -4270,8 +3180,6 @@ static bool fwd_ds_plan(const ssip_conv_desc* d, const ssip_conv_desc* dds, int 
     return false;
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp) || stem_plan(d, dtype, hp)) return false;
-  HbPlan hb;
-  if (hb_plan(MODE_FWD, d, dtype, hb)) return false;
   if (plan_conv(MODE_FWD, d, 2, pl) != SSIP_OK || pl.conv1) return false;
   return pl.stages == 2 || pl.stages == 3;
 }
@@ -4310,8 +3218,6 @@ int ssip_conv_fwd_partial_tiles(const ssip_conv_desc* d, int dtype) {
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp)) return hp.G * HALO_WMW;
   if (stem_plan(d, dtype, hp)) return hp.G * HALO_WMW;
-  HbPlan hb;
-  if (hb_plan(MODE_FWD, d, dtype, hb)) return hb.G * HALO_WMW;
   Plan pl;
   if (plan_conv(MODE_FWD, d, elem_bytes_of(dtype), pl) != SSIP_OK) return -1;
   if (pl.stages > 0 && !pl.conv1 && d->R * d->S > 32) fallback_regstaged(pl);
@@ -4347,9 +3253,6 @@ int ssip_conv_dgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
   HaloPlan hp;
   if (halo_plan(MODE_DGRAD, d, dtype, hp))
     return launch_halo(MODE_DGRAD, d, hp, dy, w_crsk, dx, dx_add, nullptr, (hipStream_t)stream);
-  HbPlan hb;
-  if (hb_plan(MODE_DGRAD, d, dtype, hb))
-    return launch_hb(MODE_DGRAD, d, hb, dy, w_crsk, dx, dx_add, nullptr, (hipStream_t)stream);
   pl.args.A = dy; pl.args.B = w_crsk; pl.args.out = dx; pl.args.add = dx_add;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
@@ -4587,18 +3490,8 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
   h.dp_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64 * 2);
   h.ix_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64);
   h.N = d->N; h.H = d->H; h.W = d->W; h.P = d->P; h.Q = d->Q; h.P2 = P2; h.Q2 = Q2; h.tiles = hp.tiles;
-  {
-    static const int diag = getenv("SSIP_STEM_DIAG") ? atoi(getenv("SSIP_STEM_DIAG")) : 0;
-    h.diag = diag & 11;
-    if (diag & 4) h.x_bytes = h.y_bytes = h.dp_bytes = h.ix_bytes = 0;  // zero-extent: no memory traffic
-  }
   hipStream_t st = (hipStream_t)stream;
-  // SSIP_STEM_BW=1: the kernel with every wave in both halves (A/B)
-  static const int v1 = getenv("SSIP_STEM_BW") ? atoi(getenv("SSIP_STEM_BW")) : 0;
-  if (v1 == 1)
-    hipLaunchKernelGGL(conv_stem_bwd_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
-  else
-    hipLaunchKernelGGL(conv_stem_bwd_wgrad2_kernel, dim3(hp.G), dim3(768), 0, st, h);
+  hipLaunchKernelGGL(conv_stem_bwd_wgrad2_kernel, dim3(hp.G), dim3(768), 0, st, h);
   int rc = ::ssip::check_launch("conv_stem_bwd_wgrad");
   if (rc) return rc;
   const long total4 = 64L * 224 / 4;
@@ -4629,11 +3522,6 @@ int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* bu
   }
   if (m == MODE_DGRAD && halo_plan(MODE_DGRAD, d, dtype, hp)) {
     snprintf(buf, buflen, "halo<dgrad,TR=%d,G=%d>", hp.TR, hp.G);
-    return SSIP_OK;
-  }
-  HbPlan hb;
-  if ((m == MODE_FWD || m == MODE_DGRAD) && hb_plan(m, d, dtype, hb)) {
-    snprintf(buf, buflen, "hb<%s,%d,TM=%d,G=%d>", mname[mode], hb.BN, hb.tm, hb.G);
     return SSIP_OK;
   }
   if (m == MODE_WGRAD && stem_wg_plan(d, dtype, hp)) {

@@ -12,17 +12,10 @@ constexpr int FIN_NT = 256;  // threads of a finalize workgroup
 constexpr int FIN_PT = 8;
 constexpr int FIN_SMAX = 64;
 
-// (SSIP_FIN_NT=64: one-wave, LDS-free finalize workgroups, an A/B option:
-// 6.52 vs 6.48 ms/step, 3 + 3 runs, the blocking in the step trace is the
-// halo kernels' register files, not their LDS)
-static inline int fin_nt() {
-  static const int nt = getenv("SSIP_FIN_NT") && atoi(getenv("SSIP_FIN_NT")) == 64 ? 64 : FIN_NT;
-  return nt;
-}
-// (SSIP_FIN_PT: records per thread before a split, a tuning override)
+// (one-wave LDS-free finalize workgroups, an A/B option in round 3, were no
+// faster: 6.52 vs 6.48 ms/step; r3-variants branch)
 static inline int fin_splits(long tiles) {
-  static const long pt = getenv("SSIP_FIN_PT") ? std::max(1, atoi(getenv("SSIP_FIN_PT"))) : FIN_PT;
-  long s = (tiles + fin_nt() * pt - 1) / (fin_nt() * pt);
+  long s = (tiles + (long)FIN_NT * FIN_PT - 1) / ((long)FIN_NT * FIN_PT);
   return (int)(s < 1 ? 1 : (s > FIN_SMAX ? FIN_SMAX : s));
 }
 // floats the split finalize needs behind `records` floats of records (vals

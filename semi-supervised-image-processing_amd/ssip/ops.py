@@ -158,7 +158,7 @@ _plan_cache = {}
 
 
 def _plan_env():
-    return (os.environ.get("SSIP_HALO"), os.environ.get("SSIP_CONV_FORCE"), os.environ.get("SSIP_HB"))
+    return (os.environ.get("SSIP_HALO"), os.environ.get("SSIP_CONV_FORCE"))
 
 
 def conv_fwd_partial_floats(g: ConvGeom) -> int:

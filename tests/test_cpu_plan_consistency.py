@@ -1,11 +1,12 @@
 """CPU: the library's kernel choice for a conv geometry and the BatchNorm
 record sizing derived from it agree on every call (host planning only, no
-device).  A persistent forward kernel (halo / hb) writes one record per
+device).  A persistent forward kernel (halo) writes one record per
 (channel, workgroup, wave row): G * 8 per channel; the partial buffer the
 engine allocates (ssip_conv_fwd_partial_floats) must hold every record the
 launched kernel writes, on the first call and on repeated (cached) calls.
-Regression: the hb plan cache once answered a repeated call differently
-from the first one (layer-4 shapes), and the forward overran its records."""
+Regression: a persistent kernel's plan cache once answered a repeated call
+differently from the first one (layer-4 shapes), and the forward overran its
+records (that kernel, conv_hb, is now on the r3-variants branch only)."""
 import re
 
 import pytest
@@ -33,7 +34,7 @@ def test_fwd_records_fit(n, C, H, K, st):
     assert len(tiles) == 1
     t = tiles.pop()
     m = re.search(r"G=(\d+)", name)
-    if name.startswith(("hb<", "halo<")):
+    if name.startswith("halo<"):
         assert m and t == int(m.group(1)) * 8, (name, t)
     floats = int(ops._lib.lib().ssip_conv_fwd_partial_floats(g.desc()))
     assert floats >= t * K * 3, (name, t, floats)

@@ -199,3 +199,12 @@ def test_stem_bs256(dev):
     torch.cuda.synchronize()
     assert torch.equal(coef, coef2) and torch.equal(dg, dg2) and torch.equal(db, db2)
     assert (dw1 - dw0).abs().max().item() <= 2e-3 * dw0.abs().max().item()
+    # the fused kernel (conv_stem_bwd_wgrad2: dy formed per tile in LDS, never
+    # stored) directly against torch's fp32 weight gradient of the materialised
+    # bf16 dy: the unfused wgrad reads exactly that dy (1e-4, summation order);
+    # the fused one forms the same bf16 values with the same coefficients, up to
+    # fma contraction in a few elements (2e-3)
+    ref_w1 = torch.nn.grad.conv2d_weight(x, (K, C, 7, 7), dyb.float().permute(0, 3, 1, 2).cpu(), stride=2, padding=3)
+    scale_w1 = ref_w1.abs().max().item()
+    assert (dw0.cpu() - ref_w1).abs().max().item() <= 1e-4 * scale_w1
+    assert (dw1.cpu() - ref_w1).abs().max().item() <= 2e-3 * scale_w1

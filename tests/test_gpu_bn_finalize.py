@@ -1,7 +1,7 @@
 """BatchNorm finalize (forward statistics and backward coefficients) over
 record counts either side of the split point (more than 2048 records per
 channel are merged by several 256-thread workgroups plus a one-wave merge
-pass; 512 with SSIP_FIN_NT=64's one-wave workgroups).  Reference: the same records merged on the host in float64 (Chan's
+pass).  Reference: the same records merged on the host in float64 (Chan's
 pairwise formula for {count, sum, M2}; plain sums for the backward), i.e. the
 batch mean / biased variance torchvision's BatchNorm2d uses
 (src/training/common.py:380 `model(inputs)` in train mode).  Tolerance:

@@ -39,11 +39,8 @@ def _stats(g, part, dt, dev):
     return stats[0].cpu(), (1 / stats[1].cpu().double() ** 2 - 1e-5)
 
 
-@pytest.mark.parametrize("waves", ["8", "4", "16"])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_halo_fwd(dev, shape, waves, monkeypatch):
-    """Every SSIP_HALO_WAVES variant (they share the 8-slot BN record layout)."""
-    monkeypatch.setenv("SSIP_HALO_WAVES", waves)
+def test_halo_fwd(dev, shape, monkeypatch):
     torch.manual_seed(10)
     N, C, H, W, K = shape
     dt = torch.bfloat16
@@ -77,11 +74,9 @@ def test_halo_fwd(dev, shape, waves, monkeypatch):
     assert _relerr(var_h, var_0) < 1e-4
 
 
-@pytest.mark.parametrize("waves", ["8", "4", "16"])
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("add", ["none", "separate", "in_place"])
-def test_halo_dgrad(dev, shape, add, waves, monkeypatch):
-    monkeypatch.setenv("SSIP_HALO_WAVES", waves)
+def test_halo_dgrad(dev, shape, add, monkeypatch):
     torch.manual_seed(11)
     N, Cr, H, W, Kc = shape
     # dgrad of a conv with C_in = Kc (the output columns) and K_out = 64 (the reduction)
@@ -116,25 +111,6 @@ def test_halo_dgrad(dev, shape, add, waves, monkeypatch):
     dx0 = run()
     assert torch.equal(dx, dx0)
     assert _relerr(dx.cpu(), ref) < 1e-2
-
-
-@pytest.mark.parametrize("bad", ["7", "0", "", "8x"])
-def test_halo_waves_rejects_other_values(dev, bad, monkeypatch):
-    """SSIP_HALO_WAVES accepts exactly 4, 8 or 16 (empty = default 8)."""
-    monkeypatch.delenv("SSIP_HALO", raising=False)
-    monkeypatch.setenv("SSIP_HALO_WAVES", bad)
-    g = ConvGeom(2, 56, 56, 64, 64, 3, 3, 1, 1, 64, 3)
-    dt = torch.bfloat16
-    x = torch.zeros((2, 56, 56, 64), device=dev, dtype=dt)
-    w = torch.zeros((64, 3, 3, 64), device=dev, dtype=dt)
-    y = torch.empty_like(x)
-    part = torch.empty(ops.conv_fwd_partial_floats(g), device=dev)
-    if bad == "":
-        ops.conv_fwd(g, x, w, y, part)
-        torch.cuda.synchronize()
-        return
-    with pytest.raises(RuntimeError, match="SSIP_HALO_WAVES"):
-        ops.conv_fwd(g, x, w, y, part)
 
 
 def test_halo_partial_tiles_is_workgroup_count(dev, monkeypatch):

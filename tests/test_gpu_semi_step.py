@@ -163,6 +163,19 @@ def _rel_l2(a, b):
 def test_semi_step_bf16_224_matches_oracle(dev):
     """The benchmarked configuration's step in bf16 (224x224, 16 labelled +
     16 unlabelled) against the float64 oracle on the same images and view
+    parameters (_bf16_step_vs_oracle)."""
+    _bf16_step_vs_oracle(dev, "resnet18", 224, 16, 16, seed=5)
+
+
+def test_semi_step_bf16_r50_512_matches_oracle(dev):
+    """BASELINE config 5's step (ResNet-50, 512x512) in bf16 -- every R50 kernel
+    at its own image size, the stem included -- on 2 labelled + 2 unlabelled
+    images against the float64 oracle (_bf16_step_vs_oracle)."""
+    _bf16_step_vs_oracle(dev, "resnet50", 512, 2, 2, seed=6)
+
+
+def _bf16_step_vs_oracle(dev, arch, S, Bl, Bu, seed):
+    """One bf16 SemiStep against the float64 oracle on the same images and view
     parameters.  Tolerances are DERIVED, per quantity, from a CPU run of the
     same oracle with the engine's bf16 storage emulated (oracle/bf16_emulate:
     bf16 conv inputs / weights / outputs and bf16 activation gradients):
@@ -179,8 +192,8 @@ def test_semi_step_bf16_224_matches_oracle(dev):
     logits are not within the tolerance of a tie."""
     from oracle.bf16_emulate import emulate_bf16
 
-    S, Bl, Bu, tau, lr = 224, 16, 16, 0.5, 1e-4
-    rng = np.random.default_rng(5)
+    tau, lr = 0.5, 1e-4
+    rng = np.random.default_rng(seed)
     x_l = rng.integers(0, 256, (Bl, S, S, 3), dtype=np.uint8)
     x_u = rng.integers(0, 256, (Bu, S, S, 3), dtype=np.uint8)
     y_l = torch.from_numpy(rng.integers(0, 2, Bl))
@@ -190,10 +203,10 @@ def test_semi_step_bf16_224_matches_oracle(dev):
     ds = [draw_strong_params(S, g) for _ in range(Bu)]
 
     torch.manual_seed(0)
-    ref = tvm.resnet18()
-    ref.fc = torch.nn.Linear(512, 2)
+    ref = getattr(tvm, arch)()
+    ref.fc = torch.nn.Linear(ref.fc.in_features, 2)
     torch.manual_seed(0)
-    mine = replace_fc(SSIPResNet("resnet18", num_classes=1000, dtype="bf16"), 2).to(dev)
+    mine = replace_fc(SSIPResNet(arch, num_classes=1000, dtype="bf16"), 2).to(dev)
     step = SemiStep(mine, lr=lr, weight_decay=1e-4, tau=tau, lambda_u=1.0, image_size=S)
     params = (encode_params(dl, S, S), encode_params(dw, S, S), encode_params(ds, S, S))
     st = step(torch.from_numpy(x_l).to(dev), y_l.to(dev), torch.from_numpy(x_u).to(dev), params)

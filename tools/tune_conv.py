@@ -11,21 +11,11 @@ sys.path.insert(0, os.path.join(ROOT, "semi-supervised-image-processing_amd"))
 import torch  # noqa: E402
 from ssip import ops  # noqa: E402
 
-FD = [(256, 128, 4, 2, 3), (256, 128, 4, 2, 2), (256, 64, 4, 1, 2), (256, 64, 4, 1, 3), (256, 64, 4, 2, 2),
-      (256, 64, 4, 2, 3), (128, 128, 2, 2, 2), (128, 128, 2, 2, 3), (128, 128, 4, 2, 2), (128, 128, 4, 2, 3),
-      (128, 64, 2, 2, 2), (128, 64, 2, 2, 3), (128, 64, 2, 1, 2), (128, 64, 4, 2, 2), (128, 128, 4, 4, 2),
-      (256, 128, 4, 4, 2), (128, 64, 4, 2, 3), (128, 128, 4, 4, 3), (256, 128, 4, 4, 3),
-      (256, 128, 2, 2, 2), (512, 64, 4, 1, 2), (256, 256, 2, 2, 2), (256, 256, 4, 2, 2), (512, 64, 8, 1, 2),
-      (256, 128, 4, 2, 5), (512, 64, 8, 1, 5), (128, 128, 4, 2, 5), (256, 64, 8, 1, 5),
-      (256, 128, 4, 2, 0), (256, 64, 4, 2, 0), (128, 128, 2, 2, 0), (128, 64, 2, 2, 0), (256, 256, 2, 4, 8)]
-WG = [(128, 128, 2, 2, 2), (128, 128, 2, 2, 3), (128, 128, 2, 4, 2), (128, 128, 2, 4, 3), (128, 64, 2, 2, 2),
-      (128, 64, 2, 2, 3), (128, 64, 2, 1, 2), (64, 128, 1, 4, 2), (64, 128, 1, 4, 3), (64, 128, 1, 2, 2),
-      (64, 128, 1, 8, 3), (128, 128, 4, 2, 2), (128, 128, 4, 4, 2), (128, 64, 2, 4, 2), (64, 128, 2, 4, 2),
-      (64, 128, 1, 8, 2), (128, 128, 4, 4, 3), (64, 128, 2, 4, 3), (128, 64, 2, 4, 3), (256, 128, 4, 4, 2),
-      (128, 256, 2, 2, 2), (256, 128, 2, 2, 2), (64, 256, 1, 2, 2), (256, 256, 2, 2, 2),
-      (128, 128, 2, 4, 5), (128, 128, 4, 2, 5), (256, 128, 4, 2, 5), (128, 256, 2, 4, 5), (64, 128, 2, 4, 5),
-      (64, 256, 1, 8, 5), (256, 256, 2, 4, 8),
-      (128, 128, 2, 2, 0), (128, 64, 2, 2, 0), (64, 128, 2, 2, 0)]
+# the configurations the library instantiates (csrc/conv.hip SSIP_GLDS_FD / SSIP_GLDS_WG;
+# round 3's wider sets are on the r3-variants branch) and the register-staged kernel (stages 0)
+FD = [(128, 128, 4, 2, 2), (128, 64, 4, 2, 2), (256, 256, 4, 2, 2), (128, 128, 4, 4, 3), (128, 128, 2, 2, 0),
+      (256, 128, 4, 2, 0)]
+WG = [(128, 128, 4, 2, 2), (64, 128, 2, 4, 2), (128, 128, 2, 2, 0)]
 
 
 def shapes(n):
@@ -59,7 +49,7 @@ def main():
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--wg", default="", help="wgrad configs 'bm,bn,wm,wn,st;...' (default: the built-in list)")
     ap.add_argument("--fd", default="", help="fwd/dgrad configs 'bm,bn,wm,wn,st;...' (default: the built-in list)")
-    ap.add_argument("--no-check", action="store_true", help="skip the result check (SSIP_DIAG ablation builds)")
+    ap.add_argument("--no-check", action="store_true", help="skip the result check")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16

@@ -38,6 +38,7 @@ import torch.distributed as dist  # noqa: E402
 GFLOP_PER_IMG_TRAIN = 10.64535   # R18 224² fwd+dgrad+wgrad (no stem dgrad)
 GFLOP_PER_IMG_FWD = 3.627125
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E spec peak (MI355X_MICROARCH.md; 6.29 TB/s measured copy)
 
 
 def _round_of(path: str) -> int:
@@ -342,8 +343,12 @@ def main():
     conv_flops = sum(v[0] for v in summ.values())
     conv_ms = sum(v[1] for v in summ.values())
     conv_launches = sum(v[2] for v in summ.values())
+    conv_bytes = sum(v[3] for v in summ.values())
     achieved = conv_flops / (conv_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
+    # per-launch speed of light: max(FLOPs / MFMA peak, algorithmic bytes / HBM peak)
+    # -- layer 1's 64-channel convs sit below the ridge point (~310 FLOP/B), HBM-bound
+    sol_s, meas_s = timer.sol(peak * 1e12, HBM_PEAK_BPS)
 
     # HBM traffic of the same family from the committed rocprofv3 PMC passes of
     # THIS workload (tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE, separate
@@ -414,7 +419,12 @@ def main():
                          "kernel": "conv family: conv_glds / conv_halo / conv_stem_halo / conv_halo_wgrad / "
                                    "conv_stem_bwd_wgrad (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
-                                   f"in {conv_ms:.3f} ms"},
+                                   f"in {conv_ms:.3f} ms",
+                         "sol": {"frac": round(sol_s / meas_s, 4), "sol_ms": round(sol_s * 1e3, 3),
+                                 "algorithmic_bytes": conv_bytes, "hbm_peak_gbps": HBM_PEAK_BPS / 1e9,
+                                 "note": "sum over the same launches of max(FLOPs / MFMA peak, algorithmic bytes / "
+                                         "HBM peak) divided by their measured time: the fraction of each launch's "
+                                         "own roofline (HBM-bound below ~312 FLOP/B)"}},
             "cpu_baseline": cpu,
             "sclk": sclk.summary(),
             "step_boundary": boundary,

@@ -80,27 +80,54 @@ def counters_add(counters, delta: int = 1) -> None:
 # HIP events recorded on the stream the kernels are launched on.
 # ---------------------------------------------------------------------------
 class ConvTimer:
-    def __init__(self):
-        self.records = []  # (kind, flops, start_event, end_event)
+    """HIP-event brackets around conv launches (bench.py's roofline leg).  Each
+    record keeps the launch's algorithmic FLOPs and its algorithmic bytes (every
+    operand tensor read once, every output written once), so a per-launch
+    speed-of-light time max(FLOPs / MFMA peak, bytes / HBM peak) can be formed."""
 
-    def wrap(self, kind: str, flops: int, fn, *args):
+    def __init__(self):
+        self.records = []  # (kind, flops, bytes, start_event, end_event)
+
+    def wrap(self, kind: str, flops: int, fn, *args, nbytes: int = 0):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         fn(*args)
         e.record()
-        self.records.append((kind, flops, s, e))
+        self.records.append((kind, flops, nbytes, s, e))
 
     def summary(self):
+        """kind -> [flops, ms, launches, bytes]"""
         torch.cuda.synchronize()
         out = {}
-        for kind, flops, s, e in self.records:
+        for kind, flops, nb, s, e in self.records:
             ms = s.elapsed_time(e)
-            d = out.setdefault(kind, [0, 0.0, 0])
+            d = out.setdefault(kind, [0, 0.0, 0, 0])
             d[0] += flops
             d[1] += ms
             d[2] += 1
+            d[3] += nb
         return out
+
+    def sol(self, peak_flops: float, peak_bytes: float):
+        """(sum over launches of max(flops / peak_flops, bytes / peak_bytes), measured sum), seconds"""
+        torch.cuda.synchronize()
+        sol = meas = 0.0
+        for _, flops, nb, s, e in self.records:
+            sol += max(flops / peak_flops, nb / peak_bytes)
+            meas += s.elapsed_time(e) * 1e-3
+        return sol, meas
+
+
+def _nbytes(*ts) -> int:
+    """Bytes of the distinct tensors given (None skipped, aliases counted once)."""
+    seen, n = set(), 0
+    for t in ts:
+        if t is None or t.data_ptr() in seen:
+            continue
+        seen.add(t.data_ptr())
+        n += t.numel() * t.element_size()
+    return n
 
 
 _timer = None
@@ -191,7 +218,7 @@ def conv_fwd(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Tensor
     d = g.desc()
     if _timer is not None:
         _timer.wrap("fwd", g.flops(), call, "ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial),
-                    stream_ptr())
+                    stream_ptr(), nbytes=_nbytes(x, w_krsc, y))
         return
     call("ssip_conv_fwd", d, dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial), stream_ptr())
 
@@ -220,7 +247,7 @@ def conv_fwd_ds(g: ConvGeom, x: torch.Tensor, w_krsc: torch.Tensor, y: torch.Ten
     args = ("ssip_conv_fwd_ds", g.desc(), gds.desc(), dtype_code(x), _p(x), _p(w_krsc), _p(y), _p(partial),
             _p(wds), _p(y_ds), _p(partial_ds), stream_ptr())
     if _timer is not None:
-        _timer.wrap("fwd", g.flops() + gds.flops(), call, *args)
+        _timer.wrap("fwd", g.flops() + gds.flops(), call, *args, nbytes=_nbytes(x, w_krsc, y, wds, y_ds))
         return
     call(*args)
 
@@ -246,7 +273,9 @@ def conv_dgrad(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx: torch.Te
         assert dx_add.numel() == dx.numel() and dx_add.dtype == dx.dtype
     args = ("ssip_conv_dgrad", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx), _p(dx_add), stream_ptr())
     if _timer is not None:
-        _timer.wrap("dgrad", g.flops(), call, *args)
+        # an in-place residual add (dx_add is dx) reads dx once more
+        extra = dx.numel() * dx.element_size() if dx_add is not None and dx_add.data_ptr() == dx.data_ptr() else 0
+        _timer.wrap("dgrad", g.flops(), call, *args, nbytes=_nbytes(dy, w_crsk, dx, dx_add) + extra)
         return
     call(*args)
 
@@ -262,7 +291,7 @@ def conv_dgrad_ds(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, gds: Conv
     args = ("ssip_conv_dgrad_ds", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dy_ds), _p(wds_crsk), _p(dx),
             stream_ptr())
     if _timer is not None:
-        _timer.wrap("dgrad", g.flops() + gds.flops(), call, *args)
+        _timer.wrap("dgrad", g.flops() + gds.flops(), call, *args, nbytes=_nbytes(dy, w_crsk, dy_ds, wds_crsk, dx))
         return
     call(*args)
 
@@ -300,7 +329,8 @@ def conv_dgrad_bn(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx_add: O
     args = ("ssip_conv_dgrad_bn", g.desc(), dtype_code(dy), _p(dy), _p(w_crsk), _p(dx_add), _p(zmask),
             _p(mask_bits), _p(mscale), _p(mshift), _p(y), _p(mean), _p(invstd), _p(dpre), _p(partial), stream_ptr())
     if _timer is not None:
-        _timer.wrap("dgrad", g.flops(), call, *args)
+        _timer.wrap("dgrad", g.flops(), call, *args,
+                    nbytes=_nbytes(dy, w_crsk, dx_add, zmask, mask_bits, y, dpre))
         return
     call(*args)
 
@@ -317,7 +347,8 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
     args = ("ssip_conv_wgrad", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real,
             int(accumulate), _p(workspace), nbytes, stream_ptr())
     if _timer is not None:
-        _timer.wrap("wgrad", g.flops(), call, *args)
+        # accumulate: dw is read as well as written
+        _timer.wrap("wgrad", g.flops(), call, *args, nbytes=_nbytes(dy, x, dw) + (dw.numel() * 4 if accumulate else 0))
         return
     call(*args)
 
@@ -339,7 +370,7 @@ def stem_bwd_wgrad(g: ConvGeom, dpool, idx, y, x, scale, shift, coef, dw, accumu
     args = ("ssip_stem_bwd_wgrad", g.desc(), dtype_code(y), _p(dpool), _p(idx), _p(y), _p(x), _p(scale), _p(shift),
             _p(coef), _p(dw), g.c_real, g.s_real, int(accumulate), _p(workspace), nbytes, stream_ptr())
     if _timer is not None:
-        _timer.wrap("wgrad", g.flops(), call, *args)
+        _timer.wrap("wgrad", g.flops(), call, *args, nbytes=_nbytes(dpool, idx, y, x, dw))
         return
     call(*args)
 

@@ -229,11 +229,6 @@ class SSIPResNet(nn.Module):
         # before it reads conv1.weight.grad.
         self.defer_stem_wgrad_join = False
         self._pending_side = None
-        # (SSIP_STEM_MAIN, default) the stem wgrad runs on main instead and the
-        # backward leaves the side stream caught up with main just before it:
-        # the caller may run the optimizer of every parameter but conv1 there
-        # (take_opt_side) and must join it before the next step
-        self._opt_side = None
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -284,12 +279,6 @@ class SSIPResNet(nn.Module):
         s, self._pending_side = self._pending_side, None
         if self._arena is not None and self._arena.pending_side is s:
             self._arena.pending_side = None
-        return s
-
-    def take_opt_side(self):
-        """The side stream the last backward left free beside a stem wgrad on
-        main (see defer_stem_wgrad_join), or None; clears it."""
-        s, self._opt_side = self._opt_side, None
         return s
 
     def join_pending_side(self) -> None:
@@ -678,9 +667,7 @@ def _backward(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor):
     try:
         deferred = _backward_impl(model, sv, dlogits, main, side)
     finally:
-        if deferred == "main":
-            model._opt_side = side
-        elif deferred:
+        if deferred:
             model._pending_side = side
             if model._arena is not None:
                 model._arena.pending_side = side  # AdamW.step / zero_grad join it
@@ -943,15 +930,6 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                 workspace)
         if side is None:
             ops.stem_bwd_wgrad(*args)
-        elif defer and _STEM_ON_MAIN:
-            # the stem wgrad stays on main (no stream hop ahead of the step's
-            # last kernel); main waits for every wgrad queued so far, and the
-            # side stream, caught up with main here, is free for the optimizer
-            # of every other parameter beside it (model.take_opt_side)
-            ops.wait_stream(main, side)
-            ops.wait_stream(side, main)
-            ops.stem_bwd_wgrad(*args)
-            return "main"
         else:
             ops.wait_stream(side, main)
             if defer:
@@ -972,10 +950,6 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     return defer
 
 
-
-# the deferred stem wgrad on the main stream, the optimizer beside it on the
-# side stream (0: the stem wgrad on the side stream, the optimizer on main)
-_STEM_ON_MAIN = os.environ.get("SSIP_STEM_MAIN", "1") != "0"
 
 def _ds_dgrad_fusable(g: ConvGeom, gds: ConvGeom) -> bool:
     """conv1 and the downsample of a block read the same input and produce the

@@ -34,7 +34,8 @@ from .resnet import DeviceImages, SSIPResNet
 
 
 # the weight refresh on the side stream beside the train views' augment
-# (SSIP_PREP_SIDE=0: on main ahead of both)
+# (SSIP_PREP_SIDE=0: on main ahead of both; round 4 re-measured it, 3 + 3
+# alternated runs on one box: 6.403 vs 6.416 ms/step, each pair in its favour)
 _PREP_SIDE = os.environ.get("SSIP_PREP_SIDE", "1") != "0"
 
 
@@ -294,17 +295,9 @@ class SemiStep:
         as it drains rather than beside it: profiles/r2_step_streams.txt.)"""
         m = self.model
         late = {id(m.conv1.weight)}
-        oside = m.take_opt_side()
-        if oside is not None:
-            # the stem wgrad is on main: every other update on the side stream
-            # beside it (this launch advances the device schedule), conv1's
-            # after both, on main
-            main = torch.cuda.current_stream()
-            with torch.cuda.stream(oside):
-                self.opt.step(grad_scale=scale, skip=late, join_pending=False)
-            ops.wait_stream(main, oside)
-            self.opt.step(grad_scale=scale, only=late, sched_step=False)
-            return
+        # (the stem wgrad on main with the other updates on the side stream,
+        # round 3's SSIP_STEM_MAIN: 6.399 vs 6.395 ms/step over 3 + 3 alternated
+        # runs, no gain -- the simpler layout stays)
         pend = m.take_pending_side()
         if pend is None:
             self.opt.step(grad_scale=scale)

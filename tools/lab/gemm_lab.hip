@@ -89,14 +89,19 @@ __global__ void __launch_bounds__(64 * NW, 1) intake_kernel(const __bf16* A, con
 // ---------------------------------------------------------------------------
 // GEMM 256x256 tile, 2-stage LDS-DMA ring
 // ---------------------------------------------------------------------------
-template <int WM, int WN, int SCHED>
-__global__ void __launch_bounds__(64 * WM * WN, (WM * WN) / 4) gemm_kernel(const __bf16* A, const __bf16* B, __bf16* C,
-                                                                             int M, int N, int K) {
-  constexpr int NW = WM * WN, BM = 256, BN = 256;
+constexpr int lab_waves(int bm, int bn, int nw) {
+  return ((163840 / (2 * (bm + bn) * 128)) * nw) / 4 > 8 ? 8 : ((163840 / (2 * (bm + bn) * 128)) * nw) / 4;
+}
+template <int WM, int WN, int SCHED, bool L2MODE = false, int BM = 256, int BN = 256>
+__global__ void __launch_bounds__(64 * WM * WN, lab_waves(BM, BN, WM * WN)) gemm_kernel(const __bf16* A,
+                                                                                         const __bf16* B, __bf16* C,
+                                                                                         int M, int N, int K) {
+  constexpr int NW = WM * WN;
   constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  constexpr int PER = 32 / NW;  // 1-KiB instructions per operand per wave per k-step
+  constexpr int PA = BM / 8 / NW, PB = BN / 8 / NW;  // 1-KiB instructions per operand per wave per k-step
+  constexpr int STAGE = (BM + BN) * 128;
   constexpr int EROW = BN * 2 + 16;  // epilogue staging row (bf16 + pad)
-  __shared__ __attribute__((aligned(16))) char smem[BM * EROW > 2 * 65536 ? BM * EROW : 2 * 65536];
+  __shared__ __attribute__((aligned(16))) char smem[BM * EROW > 2 * STAGE ? BM * EROW : 2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -104,19 +109,30 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN) / 4) gemm_kernel(const
   const int t = xcd_tile(blockIdx.x, gridDim.x);
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A + (long)m0 * K, (uint32_t)(min(BM, M - m0) * K * 2));
+  // L2MODE: every XCD's run of tiles re-reads two 256-row A panels (~2.4 MB
+  // per XCD at K 2304, L2-resident like the implicit GEMM's im2col rows);
+  // otherwise each tile streams its own rows (HBM)
+  const long arow = L2MODE ? (long)(((t / 32) * 2 + (t & 1)) % (M / 256)) * BM : (long)m0;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A + arow * K, (uint32_t)(min(BM, M - m0) * K * 2));
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(B + (long)n0 * K, (uint32_t)(BN * K * 2));
   const int row0 = 8 * wave + (lane >> 3);
   const uint32_t off = (uint32_t)((row0 * K + (((lane & 7) ^ ((row0 >> 1) & 7)) * 8)) * 2);
   const int nk = K / 64;
 
+  // (SCHED & 8: issued every k-step, the one past the end reading zeros
+  // (out-of-extent offsets) into the idle slot, so it sits in the MFMA block)
   auto issue = [&](int ks) {
-    char* st = smem + (ks & 1) * 65536;
+    char* st = smem + (ks & 1) * STAGE;
+    const bool past = ks >= nk;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
+    for (int i = 0; i < PA; ++i) {
       const uint32_t so = (uint32_t)((8 * NW * i) * K * 2 + ks * 128);
-      blds16(rsA, off, so, st + (wave + NW * i) * 1024);
-      blds16(rsB, off, so, st + 32768 + (wave + NW * i) * 1024);
+      blds16(rsA, past ? 0xFFFFFFF0u : off, past ? 0u : so, st + (wave + NW * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const uint32_t so = (uint32_t)((8 * NW * i) * K * 2 + ks * 128);
+      blds16(rsB, past ? 0xFFFFFFF0u : off, past ? 0u : so, st + BM * 128 + (wave + NW * i) * 1024);
     }
   };
 
@@ -126,15 +142,19 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN) / 4) gemm_kernel(const
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  if constexpr ((SCHED & 4) != 0) {
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   issue(0);
   for (int ks = 0; ks < nk; ++ks) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    const char* As = smem + (ks & 1) * 65536;
-    const char* Bs = As + 32768;
-    if (ks + 1 < nk) issue(ks + 1);
+    const char* As = smem + (ks & 1) * STAGE;
+    const char* Bs = As + BM * 128;
+    if constexpr ((SCHED & 8) == 0) {
+      if (ks + 1 < nk) issue(ks + 1);
+    }
     bf16x8 fa[2][FM], fb[2][FN];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    auto readh = [&](int h) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * WTM + i * 16 + (lane & 15);
@@ -145,17 +165,35 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN) / 4) gemm_kernel(const
         const int r = wn * WTN + j * 16 + (lane & 15);
         fb[h][j] = *reinterpret_cast<const bf16x8*>(Bs + ktile_off(r, 4 * h + (lane >> 4)));
       }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
+    };
+    auto mmah = [&](int h) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[h][j], acc[i][j], 0, 0, 0);
-    if constexpr (SCHED == 1) {
-      // DMA issue spread over the MFMA stream: one 1-KiB piece per MFMA group
-      constexpr int NDMA = 2 * PER, NMF = 2 * FM * FN;
+    };
+    if constexpr ((SCHED & 8) != 0) {  // reads, then the DMA (source order lets it sink among the MFMAs)
+      readh(0);
+      readh(1);
+      issue(ks + 1);
+      mmah(0);
+      mmah(1);
+    } else if constexpr ((SCHED & 2) != 0) {  // both halves' fragments requested before the first MFMA
+      readh(0);
+      readh(1);
+      mmah(0);
+      mmah(1);
+    } else {  // the production order: half 0 read, its MFMAs, half 1 read, its MFMAs
+      readh(0);
+      mmah(0);
+      readh(1);
+      mmah(1);
+    }
+    if constexpr ((SCHED & 1) != 0) {
+      // every fragment read first, then the MFMAs, the DMA issue (SCHED & 8:
+      // in this block) spread over them: one 1-KiB piece per MFMA group
+      constexpr int NDMA = PA + PB, NMF = 2 * FM * FN;
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * (FM + FN), 0);  // fragment reads first
 #pragma unroll
       for (int g = 0; g < NDMA; ++g) {
@@ -165,6 +203,7 @@ __global__ void __launch_bounds__(64 * WM * WN, (WM * WN) / 4) gemm_kernel(const
     }
   }
   // epilogue: each wave stages its tile as bf16 in LDS, then 16-B row stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -206,12 +245,13 @@ static float time_ms(F launch, int iters) {
   return ms / iters;
 }
 
-template <int WM, int WN, int SCHED>
+template <int WM, int WN, int SCHED, bool L2MODE = false, int BM = 256, int BN = 256>
 static void run_gemm(const char* name, const __bf16* dA, const __bf16* dB, __bf16* dC, int M, int N, int K,
                      const std::vector<__bf16>& hA, const std::vector<__bf16>& hB, int iters) {
-  const int tiles = ((M + 255) / 256) * (N / 256);
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
   auto go = [&] {
-    hipLaunchKernelGGL((gemm_kernel<WM, WN, SCHED>), dim3(tiles), dim3(64 * WM * WN), 0, 0, dA, dB, dC, M, N, K);
+    hipLaunchKernelGGL((gemm_kernel<WM, WN, SCHED, L2MODE, BM, BN>), dim3(tiles), dim3(64 * WM * WN), 0, 0, dA, dB,
+                       dC, M, N, K);
   };
   go();
   CK(hipGetLastError());
@@ -222,9 +262,15 @@ static void run_gemm(const char* name, const __bf16* dA, const __bf16* dB, __bf1
   double maxrel = 0;
   for (int s = 0; s < 512; ++s) {
     const int m = (int)((s * 2654435761u) % (unsigned)M), n = (int)((s * 40503u + 17) % (unsigned)N);
+    int am = m;
+    if (L2MODE) {  // the A row this output row read: tile t's panel (t = the remapped tile index)
+      const int tiles_n = N / BN;
+      const int t = (m / BM) * tiles_n + n / BN;
+      am = (((t / 32) * 2 + (t & 1)) % (M / 256)) * BM + m % BM;
+    }
     double ref = 0, mag = 0;
     for (int k = 0; k < K; ++k) {
-      const double p = (double)bf2f(hA[(size_t)m * K + k]) * bf2f(hB[(size_t)n * K + k]);
+      const double p = (double)bf2f(hA[(size_t)am * K + k]) * bf2f(hB[(size_t)n * K + k]);
       ref += p;
       mag += fabs(p);
     }
@@ -269,21 +315,18 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dA, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(dB, hB.data(), hB.size() * 2, hipMemcpyHostToDevice));
 
-  run_intake<4, 1, 0>(dA, dB, K, 256, sink, iters);
-  run_intake<4, 2, 0>(dA, dB, K, 256, sink, iters);
-  run_intake<4, 3, 0>(dA, dB, K, 256, sink, iters);
-  run_intake<8, 1, 0>(dA, dB, K, 256, sink, iters);
-  run_intake<8, 2, 0>(dA, dB, K, 256, sink, iters);
-  run_intake<8, 3, 0>(dA, dB, K, 256, sink, iters);
-  run_intake<4, 2, 1>(dA, dB, K, 256, sink, iters);
-  run_intake<8, 2, 1>(dA, dB, K, 256, sink, iters);
-  run_intake<4, 2, 0>(dA, dB, K, 196, sink, iters);
-
-  run_gemm<4, 2, 0>("gemm 8w(4x2) 64x128", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<2, 4, 0>("gemm 8w(2x4) 128x64", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<2, 2, 0>("gemm 4w(2x2) 128x128", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<2, 2, 1>("gemm 4w(2x2) 128x128 ilv", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 1>("gemm 8w(4x2) 64x128 ilv", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<2, 2, 0>("gemm 4w l3-size", dA, dB, dC, 50176, N, K, hA, hB, iters);
+  // L2-resident A (two panels per XCD), the implicit GEMM's regime
+  run_gemm<4, 2, 0, true>("256 8w(4x2) prod order", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 1, true>("256 8w(4x2) reads first", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 9, true>("256 8w(4x2) rf+dma ilv", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 13, true>("256 8w(4x2) rf+dma+prio", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<2, 4, 1, true>("256 8w(2x4) reads first", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<2, 4, 9, true>("256 8w(2x4) rf+dma ilv", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 0, true, 128, 128>("128 8w(4x2) prod order", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 1, true, 128, 128>("128 8w(4x2) reads first", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 9, true, 128, 128>("128 8w(4x2) rf+dma ilv", dA, dB, dC, M, N, K, hA, hB, iters);
+  run_gemm<4, 2, 0, true, 128, 128>("128 8w(4x2) prod N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  run_gemm<4, 2, 1, true, 128, 128>("128 8w(4x2) rf N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  run_gemm<4, 2, 9, true, 128, 128>("128 8w(4x2) rf+dma N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
   return 0;
 }

@@ -41,7 +41,7 @@ def main():
         step(x_l, y_l, x_u)
         ops.set_conv_timer(None)
         torch.cuda.synchronize()
-        runs.append([(k, f, s.elapsed_time(e) * 1e3) for k, f, s, e in t.records])
+        runs.append([(k, f, s.elapsed_time(e) * 1e3) for k, f, _, s, e in t.records])
     tot_f = tot_us = 0.0
     by_kind = {}
     for i, (k, f, _) in enumerate(runs[0]):

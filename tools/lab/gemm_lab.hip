@@ -315,18 +315,16 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dA, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(dB, hB.data(), hB.size() * 2, hipMemcpyHostToDevice));
 
-  // L2-resident A (two panels per XCD), the implicit GEMM's regime
-  run_gemm<4, 2, 0, true>("256 8w(4x2) prod order", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 1, true>("256 8w(4x2) reads first", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 9, true>("256 8w(4x2) rf+dma ilv", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 13, true>("256 8w(4x2) rf+dma+prio", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<2, 4, 1, true>("256 8w(2x4) reads first", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<2, 4, 9, true>("256 8w(2x4) rf+dma ilv", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 0, true, 128, 128>("128 8w(4x2) prod order", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 1, true, 128, 128>("128 8w(4x2) reads first", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 9, true, 128, 128>("128 8w(4x2) rf+dma ilv", dA, dB, dC, M, N, K, hA, hB, iters);
-  run_gemm<4, 2, 0, true, 128, 128>("128 8w(4x2) prod N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
-  run_gemm<4, 2, 1, true, 128, 128>("128 8w(4x2) rf N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
-  run_gemm<4, 2, 9, true, 128, 128>("128 8w(4x2) rf+dma N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  // L2-resident A (two panels per XCD), the implicit GEMM's regime.  Layer-2-like
+  // shape (N 128, K 1152): 128x128 (2 per CU) against 256x128 (1 per CU)
+  run_gemm<4, 2, 0, true, 128, 128>("128x128 prod  N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  run_gemm<4, 2, 1, true, 128, 128>("128x128 rf    N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  run_gemm<4, 2, 0, true, 256, 128>("256x128 prod  N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  run_gemm<4, 2, 1, true, 256, 128>("256x128 rf    N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  run_gemm<2, 4, 1, true, 256, 128>("256x128 2x4rf N128", dA, dB, dC, M, 128, K / 2, hA, hB, iters);
+  // layer-3-like (N 256, K 2304) at 196 tiles
+  run_gemm<4, 2, 1, true>("256x256 rf l3 M", dA, dB, dC, 50176, N, K, hA, hB, iters);
+  run_gemm<4, 2, 1, true, 128, 128>("128x128 rf l3 M", dA, dB, dC, 50176, N, K, hA, hB, iters);
+  run_gemm<4, 2, 1, true, 256, 128>("256x128 rf l3 M", dA, dB, dC, 50176, N, K, hA, hB, iters);
   return 0;
 }

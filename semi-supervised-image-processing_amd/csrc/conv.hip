@@ -1338,16 +1338,6 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
 #pragma unroll
         for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
     }
-    // every fragment read of the k-step (both k-halves) is issued before its
-    // first MFMA: the compiler's own order interleaves them and stalls MFMAs on
-    // their reads' counted waits (tools/lab/gemm_lab.hip, L2-resident plain
-    // GEMM, 256 tiles: 256x256 1124 -> 1185 TF/s, 128x128 975 -> 1072 TF/s;
-    // profiles/r4_lab.txt).  Not with the fused BN-backward epilogue (POST),
-    // whose operands stay in registers through the loop: spills at 128 VGPRs.
-    if constexpr (!POST) {
-      __builtin_amdgcn_sched_group_barrier(0x100, (WG ? 4 : 2) * (FM + FN), 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN, 0);
-    }
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
   }
   __syncthreads();

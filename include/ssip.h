@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 9
+#define SSIP_ABI_VERSION 10
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -130,6 +130,15 @@ int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d);
 /* dw_kcrs (fp32, torchvision layout [K][c_real][R][s_real]) (+)= dW */
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
                     int s_real, int accumulate, void* workspace, int64_t workspace_bytes, void* stream);
+/* The same with a workgroup budget for the split-K grid of the LDS-DMA wgrad
+ * (ABI 10): split count = ceil(max_workgroups / output tiles), for a wgrad
+ * that shares the chip with another stream's kernels (the backward's side
+ * stream beside the dgrad / BN-backward chain: one workgroup per CU leaves
+ * each CU room for the main stream); 0 = ssip_conv_wgrad's full-chip grid.
+ * Same result up to the fp32 order of the split sum (fixed for a budget). */
+int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs,
+                           int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
+                           int max_workgroups, void* stream);
 
 /* Name of the kernel a pass selects for this geometry (mode 0 = fwd,
  * 1 = dgrad, 2 = wgrad), e.g. "glds<fwd,256x256,4x2,2,splits=1>" or

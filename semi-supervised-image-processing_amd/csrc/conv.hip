@@ -2693,7 +2693,7 @@ static int apply_force(int mode, int elem_bytes, Plan& pl) {
   return SSIP_OK;
 }
 
-static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl) {
+static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl, int wg_budget = 0) {
   SSIP_REQUIRE(desc_ok(d), SSIP_ERR_ARG, "bad conv descriptor");
   pl.mode = mode;
   pl.conv1 = (d->C == 4);
@@ -2747,8 +2747,15 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
     const int cap_bytes = (int)std::max<long>(1, (64l << 20) / slab_split);
     const int max_splits = std::max(1, std::min(cap_bytes, total_ks / 16));
     int splits = 1;
-    if (const char* e = getenv("SSIP_WGRAD_BLOCKS")) {  // tuning override: target workgroup count
+    if (const char* e = getenv("SSIP_WGRAD_BLOCKS"); e && e[0]) {  // tuning override: target workgroup count
       splits = std::min(max_splits, ceil_div(std::max(1, atoi(e)), tiles));
+    } else if (pl.stages > 0 && wg_budget > 0) {
+      // a wgrad sharing the chip (ssip_conv_wgrad_budget): ResNet-18 train
+      // step with the side-stream wgrads at one workgroup per CU, two A/Bs of
+      // 3 + 3 alternated runs: 6.341 vs 6.369 and 6.431 vs 6.490 ms/step
+      // (the main stream's BN-backward passes wait less for wgrad workgroups
+      // to retire, and half the split slabs move through HBM)
+      splits = std::min(max_splits, ceil_div(wg_budget, tiles));
     } else if (pl.stages > 0) {
       const int nt = 64 * pl.wmw * pl.wnw;
       const int nbuf = std::max(2, pl.stages);
@@ -3377,8 +3384,16 @@ int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d) {
 
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
                     int s_real, int accumulate, void* workspace, int64_t workspace_bytes, void* stream) {
+  return ssip_conv_wgrad_budget(d, dtype, dy, x, dw_kcrs, c_real, s_real, accumulate, workspace, workspace_bytes, 0,
+                                stream);
+}
+
+int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs,
+                           int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
+                           int max_workgroups, void* stream) {
+  SSIP_REQUIRE(max_workgroups >= 0, SSIP_ERR_ARG, "ssip_conv_wgrad_budget: negative budget");
   Plan pl;
-  int rc = plan_conv(MODE_WGRAD, d, elem_bytes_of(dtype), pl);
+  int rc = plan_conv(MODE_WGRAD, d, elem_bytes_of(dtype), pl, max_workgroups);
   if (rc) return rc;
   SSIP_REQUIRE(dy && x && dw_kcrs && workspace, SSIP_ERR_ARG, "ssip_conv_wgrad: null pointer");
   const int64_t need = (int64_t)pl.splits * pl.args.M * pl.args.Ng * 4;

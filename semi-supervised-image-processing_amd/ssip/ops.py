@@ -340,12 +340,18 @@ def conv_wgrad_workspace_bytes(g: ConvGeom) -> int:
 
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool,
-               workspace: torch.Tensor) -> None:
+               workspace: torch.Tensor, max_workgroups: int = 0) -> None:
+    """max_workgroups > 0: the split-K grid of a wgrad sharing the chip with
+    another stream (ssip_conv_wgrad_budget); 0: the full-chip grid."""
     assert dy.numel() == g.N * g.P * g.Q * g.K and x.numel() == g.N * g.H * g.W * g.C
     assert dw.dtype == torch.float32 and dw.numel() == g.K * g.c_real * g.R * g.s_real
     nbytes = workspace.numel() * workspace.element_size()
-    args = ("ssip_conv_wgrad", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real,
-            int(accumulate), _p(workspace), nbytes, stream_ptr())
+    if max_workgroups > 0:
+        args = ("ssip_conv_wgrad_budget", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real,
+                int(accumulate), _p(workspace), nbytes, int(max_workgroups), stream_ptr())
+    else:
+        args = ("ssip_conv_wgrad", g.desc(), dtype_code(dy), _p(dy), _p(x), _p(dw), g.c_real, g.s_real,
+                int(accumulate), _p(workspace), nbytes, stream_ptr())
     if _timer is not None:
         # accumulate: dw is read as well as written
         _timer.wrap("wgrad", g.flops(), call, *args, nbytes=_nbytes(dy, x, dw) + (dw.numel() * 4 if accumulate else 0))

@@ -633,6 +633,17 @@ WGRAD_SIDE_STREAM = os.environ.get("SSIP_WGRAD_STREAM", "1") != "0"
 _side_streams = {}
 
 
+_cus = {}
+
+
+def _cu_count(dev: torch.device) -> int:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    n = _cus.get(idx)
+    if n is None:
+        n = _cus[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return n
+
+
 def _wgrad_stream(dev: torch.device):
     if not WGRAD_SIDE_STREAM or dev.type != "cuda":
         return None
@@ -814,7 +825,8 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             return
         ops.wait_stream(side, main)
         with torch.cuda.stream(side):
-            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
+            # beside the main stream's dgrad / BN chain: one workgroup per CU
+            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace, max_workgroups=_cu_count(dev))
         dy.record_stream(side)
 
     def conv_dgrad(rec: _ConvRec, dy, out, add=None):

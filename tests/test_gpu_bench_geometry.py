@@ -138,10 +138,16 @@ def test_wgrad_bs256(dev, name, shape, kern):
     ops.conv_wgrad(g, dyh, xh, dw, False, ws)
     dwa = base.clone()
     ops.conv_wgrad(g, dyh, xh, dwa, True, ws)
+    # the side-stream grid (ssip_conv_wgrad_budget, one workgroup per CU): fewer
+    # splits, the same result up to the split sum's fp32 order
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    dwb = torch.full((K, C, R, R), float("nan"), device=dev)
+    ops.conv_wgrad(g, dyh, xh, dwb, False, ws, max_workgroups=cus)
     torch.cuda.synchronize()
     scale = ref.abs().max().item()
     assert (dw.cpu() - ref).abs().max().item() <= 1e-4 * scale, name
     assert (dwa.cpu() - base.cpu() - ref).abs().max().item() <= 1e-4 * scale + 1e-6 * base.abs().max().item(), name
+    assert (dwb.cpu() - ref).abs().max().item() <= 1e-4 * scale, name
 
 
 def test_stem_bs256(dev):

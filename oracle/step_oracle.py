@@ -16,6 +16,7 @@ Used by bench.py's `cpu_baseline` leg (timed on the GPU box's host cores).
 """
 from __future__ import annotations
 
+import sys
 import time
 from typing import Dict
 
@@ -163,13 +164,17 @@ def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2,
     x_u = rng.integers(0, 256, (Bu, size, size, 3), dtype=np.uint8)
     y_l = torch.from_numpy(rng.integers(0, 2, Bl))
     step = CpuSemiStep(arch=arch, size=size)
-    for _ in range(warmup):
+    for i in range(warmup):
+        t0 = time.perf_counter()
         step(x_l, y_l, x_u)
+        # one progress line per step on stderr: a multi-minute baseline must not look hung
+        print(f"cpu_baseline warm-up {i + 1}/{warmup}: {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     times = []
-    for _ in range(steps):
+    for i in range(steps):
         t0 = time.perf_counter()
         step(x_l, y_l, x_u)
         times.append(time.perf_counter() - t0)
+        print(f"cpu_baseline step {i + 1}/{steps}: {times[-1]:.2f} s", file=sys.stderr, flush=True)
         if budget_s > 0 and len(times) >= 3 and sum(times) >= budget_s:
             break
     dt = statistics.median(times)

@@ -13,7 +13,7 @@ shift
 extra=("$@")
 out=gpurun_out/$tag
 mkdir -p $out
-timeout -k 10 420 python bench.py "${extra[@]}" > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
+timeout -k 10 600 python bench.py "${extra[@]}" > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
 tail -1 $out/bench.log | cut -c1-300
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
   python bench.py --steps 10 --warmup 5 --no-cpu-baseline "${extra[@]}" > $out/trace.log 2>&1 || { tail -20 $out/trace.log; exit 1; }

@@ -164,10 +164,13 @@ def attach_grad_allreduce(model, optimizer) -> None:
     optimizer.dp_bucketer = bucketer
 
 
+
 def rank_sum(values: List[float]) -> List[float]:
-    """Element-wise sum over ranks (host floats)."""
+    """Element-wise sum over ranks (host floats; over RCCL the values travel
+    in a device tensor: the "nccl" backend has no CPU tensors)."""
     if world() == 1:
         return list(values)
-    t = torch.tensor(values, dtype=torch.float64)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor(values, dtype=torch.float64, device=dev)
     dist.all_reduce(t)
-    return t.tolist()
+    return t.cpu().tolist()

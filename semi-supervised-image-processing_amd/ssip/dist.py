@@ -47,6 +47,9 @@ class GradBucketer:
         self.arena = arena
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # collectives whenever a process group exists, also at world size 1
+        # (RCCL then copies in place: the one-GPU RCCL test runs this path)
+        self.active = dist.is_initialized()
         # buckets in reverse parameter order (the backward produces the last params first)
         params = list(arena.params)
         spans = [arena.span(p) for p in params]
@@ -93,7 +96,7 @@ class GradBucketer:
         if self.capture_mode:
             return
         lo, hi = self.ranges[b]
-        if self.world > 1:
+        if self.active:
             self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                                 async_op=True))
 
@@ -109,7 +112,7 @@ class GradBucketer:
         self._comm.wait_stream(torch.cuda.current_stream())
         self.handles = []
         for b in range(len(self.buckets)):
-            if self.world > 1 and any(self.params[i].requires_grad for i in self.buckets[b]):
+            if self.active and any(self.params[i].requires_grad for i in self.buckets[b]):
                 lo, hi = self.ranges[b]
                 with torch.cuda.stream(self._comm):
                     self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM,

@@ -135,7 +135,9 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
  * that shares the chip with another stream's kernels (the backward's side
  * stream beside the dgrad / BN-backward chain: one workgroup per CU leaves
  * each CU room for the main stream); 0 = ssip_conv_wgrad's full-chip grid.
- * Same result up to the fp32 order of the split sum (fixed for a budget). */
+ * The persistent layer-1 and stem wgrads (one workgroup per CU, all of its
+ * LDS) run on at most max_workgroups CUs.  Same result up to the fp32 order
+ * of the split / slab sum (fixed for a budget). */
 int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs,
                            int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
                            int max_workgroups, void* stream);

@@ -3403,6 +3403,7 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
   {
     HaloPlan hp;
     if (stem_wg_plan(d, dtype, hp)) {
+      if (max_workgroups > 0) hp.G = std::min(hp.G, max_workgroups);
       const int64_t sneed = (int64_t)hp.G * 64 * 224 * 4;
       SSIP_REQUIRE(workspace_bytes >= sneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
                    (long long)workspace_bytes, (long long)sneed);
@@ -3426,6 +3427,7 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
       return ::ssip::check_launch("wgrad_reduce");
     }
     if (halo_wg_plan(d, dtype, hp)) {
+      if (max_workgroups > 0) hp.G = std::min(hp.G, max_workgroups);  // persistent: fewer CUs, more tiles each
       const int64_t hneed = (int64_t)hp.G * 64 * 576 * 4;
       SSIP_REQUIRE(workspace_bytes >= hneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
                    (long long)workspace_bytes, (long long)hneed);

@@ -644,6 +644,25 @@ def _cu_count(dev: torch.device) -> int:
     return n
 
 
+_side_budgets = {}
+
+
+def _side_wgrad_budget(g, dtype, dev: torch.device) -> int:
+    """Grid cap of a wgrad on the side stream, beside the main stream's dgrad /
+    BN-backward chain (ssip_conv_wgrad_budget): the split-K LDS-DMA wgrads one
+    workgroup per CU (SSIP_WGRAD_BLOCKS sweep: 6.431 ms at 256 vs 6.490
+    uncapped), the persistent layer-1 wgrad -- one workgroup per CU holding all
+    of its LDS, so a main-stream kernel cannot start beside it -- half the CUs
+    (6.551 vs 6.650 ms at 100 %, 6.567 at 62 %, 6.637 at 37 %; 3 alternated
+    runs each, tools/gpu_r4_halo.sh)."""
+    key = (g, dtype, dev.index)
+    b = _side_budgets.get(key)
+    if b is None:
+        cus = _cu_count(dev)
+        b = _side_budgets[key] = cus // 2 if ops.conv_kernel_name("wgrad", g, dtype).startswith("halo_wgrad") else cus
+    return b
+
+
 def _wgrad_stream(dev: torch.device):
     if not WGRAD_SIDE_STREAM or dev.type != "cuda":
         return None
@@ -825,8 +844,8 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             return
         ops.wait_stream(side, main)
         with torch.cuda.stream(side):
-            # beside the main stream's dgrad / BN chain: one workgroup per CU
-            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace, max_workgroups=_cu_count(dev))
+            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
+                           max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev))
         dy.record_stream(side)
 
     def conv_dgrad(rec: _ConvRec, dy, out, add=None):

@@ -190,8 +190,7 @@ int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stri
   SSIP_REQUIRE((long)B * (Ho + 2 * out_pad) < 65536l * 65536l && B < 65536, SSIP_ERR_ARG,
                "ssip_augment_u8: batch too large");
   const int wp = Wo + 2 * out_pad, hp = Ho + 2 * out_pad;
-  // 4 rows per workgroup (SSIP_AUG_ROWS: tuning override)
-  static const int rows = getenv("SSIP_AUG_ROWS") ? std::max(1, atoi(getenv("SSIP_AUG_ROWS"))) : 4;
+  const int rows = 4;  // output rows per workgroup (round 2: 46.7 -> 34.2 us per launch vs one row)
   const dim3 grid((unsigned)((hp + rows - 1) / rows), (unsigned)B);
   const dim3 block((unsigned)(wp >= 256 ? 256 : ((wp + 63) / 64) * 64));
   SSIP_DISPATCH_DTYPE(dtype, T, {

@@ -2779,10 +2779,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   a.tiles_n = ceil_div(a.Ng, pl.bn);
   const int tiles_m = ceil_div(a.M, pl.bm);
   pl.grid = dim3(tiles_m * a.tiles_n, pl.splits, 1);
-  {
-    const char* e = getenv("SSIP_CONV_NO_XCD");
-    a.xcd_remap = (e && e[0] == '1') ? 0 : 1;
-  }
+  a.xcd_remap = 1;
   return SSIP_OK;
 }
 
@@ -2945,8 +2942,6 @@ static void set_phase_order(ConvArgs& a) {
 // gather as zeros.  blockIdx.y = phase; grid.x covers the largest phase.
 static void phase_split(Plan& pl, const ssip_conv_desc* d) {
   if (pl.stages == 0 || pl.conv1 || d->stride != 2) return;
-  const char* e = getenv("SSIP_CONV_NO_PHASE");
-  if (e && e[0] == '1') return;
   ConvArgs& a = pl.args;
   int max_tiles = 0;
   for (int f = 0; f < 4; ++f) {
@@ -3278,8 +3273,7 @@ int ssip_conv_dgrad_ds(const ssip_conv_desc* d, int dtype, const void* dy, const
   int rc = plan_conv(MODE_DGRAD, d, elem_bytes_of(dtype), pl);
   if (rc) return rc;
   phase_split(pl, d);
-  const bool fuse = pl.stages > 0 && pl.args.phased && d->R == 3 && d->S == 3 && d->pad == 1 && d->stride == 2 &&
-                    !getenv("SSIP_CONV_NO_DSFUSE");
+  const bool fuse = pl.stages > 0 && pl.args.phased && d->R == 3 && d->S == 3 && d->pad == 1 && d->stride == 2;
   if (!fuse) {  // two passes: the conv's dgrad, then the downsample's accumulated in place
     rc = ssip_conv_dgrad(d, dtype, dy, w_crsk, dx, nullptr, stream);
     if (rc) return rc;

@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(const WprepTable
   // remap so each XCD runs a contiguous range, which puts the R*Sp tap slices
   // of one 64x64 (k, c) tile on one XCD: they read the same KCRS cache lines
   // (a 36-B lane stride), fetched into that XCD's L2 once instead of by up
-  // to nine XCDs.  SSIP_WPREP_NO_XCD=1 (kernel arg xcd = 0) keeps the plain order.
+  // to nine XCDs.
   int b = blockIdx.x, idx = 0;
   if (tab.xcd) {
     const int nb = gridDim.x, xcd = b & 7, q = nb >> 3, r = nb & 7;
@@ -246,10 +246,7 @@ extern "C" int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* it
     tiles += ((e.K + 63) / 64) * ((e.Cp + 63) / 64) * e.R * e.Sp;
   }
   tab.tile_start[count] = tiles;
-  {
-    static const bool no_xcd = getenv("SSIP_WPREP_NO_XCD") && getenv("SSIP_WPREP_NO_XCD")[0] == '1';
-    tab.xcd = no_xcd ? 0 : 1;
-  }
+  tab.xcd = 1;
   SSIP_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(weight_prep_batch_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, tab);
   });

@@ -222,11 +222,8 @@ int ssip_plan_run(ssip_plan* plan, int segment) {
   }
   const size_t b = plan->seg_begin[segment];
   const size_t e = segment + 1 < (int)plan->seg_begin.size() ? plan->seg_begin[segment + 1] : plan->ops.size();
-  // SSIP_PLAN_INTERLEAVE=0: the recorded order (A/B)
-  const char* ev = getenv("SSIP_PLAN_INTERLEAVE");
-  const bool ilv = !(ev && ev[0] == '0');
-  if (ilv && plan->ilv_ops != plan->ops.size()) interleave_segments(plan);
-  const std::vector<Op>& seq = ilv ? plan->ilv : plan->ops;
+  if (plan->ilv_ops != plan->ops.size()) interleave_segments(plan);
+  const std::vector<Op>& seq = plan->ilv;
   for (size_t i = b; i < e; ++i) {
     const Op& op = seq[i];
     switch (op.kind) {

@@ -29,7 +29,7 @@ def abi_version_expected() -> int:
     return int(m.group(1)) if m else ABI_VERSION
 
 
-ABI_VERSION = 10  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
+ABI_VERSION = 11  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1

@@ -584,15 +584,16 @@ def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
 
 
 def adamw_sched_step(sched: torch.Tensor, beta1: float, beta2: float) -> None:
-    assert sched.dtype == torch.float64 and sched.numel() >= 4
+    assert sched.dtype == torch.float64 and sched.numel() >= 7
     call("ssip_adamw_sched_step", _p(sched), float(beta1), float(beta2), stream_ptr())
 
 
 def adamw_dev(param, grad, exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale=1.0,
               advance: bool = False) -> None:
     """advance: this launch also advances the device schedule (t, bias
-    corrections) -- the first update launch of a step; sched needs 5 slots."""
-    assert sched.dtype == torch.float64 and sched.numel() >= (5 if advance else 4)
+    corrections) -- the first update launch of a step; sched needs 7 slots
+    (ABI 11: 5-6 stage the next step's bias corrections, 0 = not staged)."""
+    assert sched.dtype == torch.float64 and sched.numel() >= (7 if advance else 4)
     call("ssip_adamw_dev", param.numel(), _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), _p(sched), float(beta1),
          float(beta2), float(eps), float(weight_decay), float(grad_scale), int(bool(advance)), stream_ptr())
 

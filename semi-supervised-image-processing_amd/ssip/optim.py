@@ -27,7 +27,7 @@ class AdamW(torch.optim.Optimizer):
         self.arena = arena
         self._flat_state = None  # (exp_avg_flat, exp_avg_sq_flat) parallel to arena.flat
         self._runs_cache: Dict[int, List[Tuple[int, int, List[torch.Tensor]]]] = {}
-        self._sched = None     # per group: fp64 device tensor {lr, t, lr/(1-b1^t), sqrt(1-b2^t)}
+        self._sched = None     # per group: fp64 device tensor {lr, t, lr/(1-b1^t), sqrt(1-b2^t), ...}
         self._sched_lr = None
         # data parallelism (src/training/distributed.attach_grad_allreduce): a
         # GradBucketer whose all-reduces step() waits for, averaging by 1/world
@@ -58,8 +58,10 @@ class AdamW(torch.optim.Optimizer):
                 if st and "step" in st:
                     t = float(st["step"])
                     break
-            # {lr, t, lr/(1-b1^t), sqrt(1-b2^t), arrival counter of the advancing launch}
-            self._sched.append(torch.tensor([group["lr"], t, 0.0, 0.0, 0.0], dtype=torch.float64, device=dev))
+            # {lr, t, lr/(1-b1^t), sqrt(1-b2^t), arrival counter of the advancing launch,
+            #  staged 1-b1^(t+1), sqrt(1-b2^(t+1)) (0: not staged yet)}
+            self._sched.append(torch.tensor([group["lr"], t, 0.0, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64,
+                                            device=dev))
             self._sched_lr.append(group["lr"])
 
     def _ensure_flat_state(self):

@@ -247,7 +247,7 @@ def test_adamw_device_schedule_fused_advance(dev):
     # the separate schedule launch, by hand
     qs = [b.clone().to(dev) for b in base]
     mv = [(torch.zeros_like(q), torch.zeros_like(q)) for q in qs]
-    scheds = [torch.tensor([lr, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64, device=dev) for lr in (1e-3, 5e-4)]
+    scheds = [torch.tensor([lr] + [0.0] * 6, dtype=torch.float64, device=dev) for lr in (1e-3, 5e-4)]
     for gs in grads:
         for gi, idx in ((0, (0, 2)), (1, (1, 3))):
             ops.adamw_sched_step(scheds[gi], 0.9, 0.999)
@@ -259,6 +259,43 @@ def test_adamw_device_schedule_fused_advance(dev):
     for k in range(4):
         assert torch.equal(ps[k].detach().cpu(), qs[k].cpu()), k
         assert _rel(ps[k].detach(), ref[k].detach()) < 1e-6, k
+
+
+@pytest.mark.parametrize("off", [0, 1, 2, 3])
+def test_adamw_vector_body_bitwise(dev, off):
+    """The AdamW kernels' 16-B vector body with its scalar head and tail (an
+    arena run at any element offset) equals the all-scalar path (taken when
+    the gradient's 16-B alignment differs from the parameter's) bit for bit,
+    for the device-schedule and the host-schedule kernels, and torch.optim.AdamW
+    to fp32 rounding, over 3 steps."""
+    n = 40_003
+    torch.manual_seed(4)
+    base = torch.randn(n + 8)
+    grads = [torch.randn(n) for _ in range(3)]
+
+    def run(goff, dev_sched):
+        P = base.clone().to(dev)
+        M, V, G = (torch.zeros(n + 8, device=dev) for _ in range(3))
+        p, m, v, g = P[off:off + n], M[off:off + n], V[off:off + n], G[goff:goff + n]
+        sched = torch.tensor([1e-3] + [0.0] * 6, dtype=torch.float64, device=dev)
+        for t, gr in enumerate(grads, 1):
+            g.copy_(gr.to(dev))
+            if dev_sched:
+                ops.adamw_dev(p, g, m, v, sched, 0.9, 0.999, 1e-8, 1e-2, advance=True)
+            else:
+                ops.adamw(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-2, t)
+        torch.cuda.synchronize()
+        return p.cpu()
+
+    ref = torch.nn.Parameter(base[off:off + n].clone())
+    topt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
+    for gr in grads:
+        ref.grad = gr.clone()
+        topt.step()
+    for dev_sched in (True, False):
+        vec, sca = run(off, dev_sched), run(off + 1, dev_sched)
+        assert torch.equal(vec, sca), dev_sched
+        assert _rel(vec, ref.detach()) < 1e-6, dev_sched
 
 
 @pytest.mark.parametrize("n", [5, 3 * 256 + 10])
@@ -274,7 +311,7 @@ def test_adamw_dev_advance_small_n(dev, n):
     topt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
     p = p0.clone().to(dev)
     m, v = torch.zeros_like(p), torch.zeros_like(p)
-    sched = torch.tensor([1e-3, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64, device=dev)
+    sched = torch.tensor([1e-3] + [0.0] * 6, dtype=torch.float64, device=dev)
     for _ in range(40):
         g = torch.randn(n)
         ref.grad = g.clone()

@@ -1404,6 +1404,48 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// The same reduction with coalesced KCRS stores, for few splits over many
+// output rows (C % 64 == 0, no channel / tap padding): one workgroup per
+// (k, 64-channel block) sums the block's R*S segments of 64 columns (16-B
+// vectors, splits in order) into LDS as [c][rs] and writes dW[k][c0 ..
+// c0+63][r][s] -- 64 R S contiguous floats -- as 16-B vectors.  (The kernel
+// above stores 4-B values R*S floats apart, a partial line per lane.)
+constexpr int WGR_T_MAXRS = 9;
+
+__global__ void __launch_bounds__(256) wgrad_reduce_t_kernel(const float* __restrict__ slab, int splits, int K,
+                                                             int Ng, int C, int RS, float* __restrict__ dw,
+                                                             int accumulate) {
+  typedef __attribute__((ext_vector_type(4))) float f4;
+  __shared__ float tile[64 * WGR_T_MAXRS];
+  const int cblocks = C >> 6;
+  const int k = blockIdx.x / cblocks, c0 = (blockIdx.x - k * cblocks) << 6;
+  const long sstride4 = (long)K * Ng / 4;
+  for (int u = threadIdx.x; u < RS * 16; u += blockDim.x) {
+    const int rs = u >> 4, cv = u & 15;
+    const f4* p = reinterpret_cast<const f4*>(slab) + ((long)k * Ng + (long)rs * C + c0 + cv * 4) / 4;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    int sp = 0;
+    for (; sp + 4 <= splits; sp += 4) {
+      const f4 a0 = p[(long)sp * sstride4], a1 = p[(long)(sp + 1) * sstride4];
+      const f4 a2 = p[(long)(sp + 2) * sstride4], a3 = p[(long)(sp + 3) * sstride4];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; sp < splits; ++sp) acc += p[(long)sp * sstride4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[(cv * 4 + e) * RS + rs] = acc[e];
+  }
+  __syncthreads();
+  f4* o = reinterpret_cast<f4*>(dw + ((long)k * C + c0) * RS);
+  for (int i = threadIdx.x; i < 16 * RS; i += blockDim.x) {
+    f4 t = {tile[4 * i], tile[4 * i + 1], tile[4 * i + 2], tile[4 * i + 3]};
+    if (accumulate) t += o[i];
+    o[i] = t;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Halo-resident 3x3 / stride 1 / pad 1 convolution over 64 reduction
 // channels: every forward conv of ResNet layer1 and every stride-1 DGRAD
@@ -3461,6 +3503,13 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
   hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, rc = launch_conv<MODE_WGRAD, T>(pl, st));
   if (rc) return rc;
+  const int RS = d->R * d->S;
+  if (c_real == d->C && s_real == d->S && d->C % 64 == 0 && RS <= WGR_T_MAXRS && pl.args.Ng == RS * d->C &&
+      pl.splits <= 32 && (long)d->K * (d->C / 64) >= 256 && (reinterpret_cast<uintptr_t>(dw_kcrs) & 15) == 0) {
+    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)(d->K * (d->C / 64))), dim3(256), 0, st,
+                       (const float*)workspace, pl.splits, d->K, pl.args.Ng, d->C, RS, dw_kcrs, accumulate);
+    return ::ssip::check_launch("wgrad_reduce_t");
+  }
   const long total4 = (long)d->K * pl.args.Ng / 4;  // Ng = R*S*C: C % 32 == 0, or the stem's 7x8x4
   int lg = 0;  // split groups: double while splits allow and the grid stays within ~1024 workgroups
   while (lg < 6 && (2 << lg) <= pl.splits && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;

@@ -197,7 +197,20 @@ __global__ void __launch_bounds__(1024) fc_bwd_weight_kernel(int B, int C, int J
   float a = 0.f;
   if (i < J * C) {
     const int j = i / C, c = i % C;
-    for (int b = bg; b < B; b += 16) a += dlogits[(long)b * J + j] * feat[(long)b * C + c];
+    // four batch rows' loads in flight per trip (a serial load chain was
+    // 21 us on the main stream at batch 256); the sum keeps the b order
+    int b = bg;
+    for (; b + 48 < B; b += 64) {
+      const float d0 = dlogits[(long)b * J + j], d1 = dlogits[(long)(b + 16) * J + j];
+      const float d2 = dlogits[(long)(b + 32) * J + j], d3 = dlogits[(long)(b + 48) * J + j];
+      const float f0 = feat[(long)b * C + c], f1 = feat[(long)(b + 16) * C + c];
+      const float f2 = feat[(long)(b + 32) * C + c], f3 = feat[(long)(b + 48) * C + c];
+      a += d0 * f0;
+      a += d1 * f1;
+      a += d2 * f2;
+      a += d3 * f3;
+    }
+    for (; b < B; b += 16) a += dlogits[(long)b * J + j] * feat[(long)b * C + c];
   }
   red[bg][cl] = a;
   __syncthreads();
@@ -207,10 +220,24 @@ __global__ void __launch_bounds__(1024) fc_bwd_weight_kernel(int B, int C, int J
     for (int g = 0; g < 16; ++g) t += red[g][cl];
     dw[i] = accumulate ? dw[i] + t : t;
   }
-  if (dbias && blockIdx.x == 0 && threadIdx.x < J) {
-    float t = 0.f;
-    for (int b = 0; b < B; ++b) t += dlogits[(long)b * J + threadIdx.x];
-    dbias[threadIdx.x] = accumulate ? dbias[threadIdx.x] + t : t;
+  if (dbias && blockIdx.x == 0) {
+    // the 16 batch groups' partial sums (b = bg mod 16, in order), combined in
+    // fixed order: no single-thread chain over the whole batch
+    for (int j0 = 0; j0 < J; j0 += 64) {
+      const int j = j0 + cl;
+      float t = 0.f;
+      if (j < J)
+        for (int b = bg; b < B; b += 16) t += dlogits[(long)b * J + j];
+      __syncthreads();
+      red[bg][cl] = t;
+      __syncthreads();
+      if (bg == 0 && j < J) {
+        float s = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) s += red[g][cl];
+        dbias[j] = accumulate ? dbias[j] + s : s;
+      }
+    }
   }
 }
 

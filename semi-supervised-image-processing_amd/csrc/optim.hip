@@ -209,15 +209,20 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(const WprepTable
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   T* krsc = static_cast<T*>(e.w_krsc);
   T* crsk = static_cast<T*>(e.w_crsk);
-#pragma unroll 4
-  for (int kk = ty; kk < 64; kk += 4) {
-    const int k = k0 + kk, c = c0 + tx;
-    float v = 0.f;
-    if (k < e.K && c < e.C && s < e.S) {
-      v = e.w_kcrs[(((long)k * e.C + c) * e.R + r) * e.S + s];
-      if (e.kscale) v *= e.kscale[k];
-    }
-    tile[kk][tx] = v;
+  // all sixteen loads of a thread in flight before the first LDS store (a
+  // partly unrolled loop paid several HBM round trips per workgroup)
+  float vals[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = k0 + ty + 4 * q, c = c0 + tx;
+    vals[q] = (k < e.K && c < e.C && s < e.S) ? e.w_kcrs[(((long)k * e.C + c) * e.R + r) * e.S + s] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = k0 + ty + 4 * q;
+    float v = vals[q];
+    if (e.kscale && k < e.K) v *= e.kscale[k];
+    tile[ty + 4 * q][tx] = v;
   }
   __syncthreads();
   if (krsc) {

@@ -314,7 +314,10 @@ def main():
     boundary = {"gap_us_median": round(gaps[len(gaps) // 2], 1), "gap_us_max": round(gaps[-1], 1),
                 "host_enqueue_ms_median": round(enq[len(enq) // 2] * 1e3, 3),
                 "note": "launch-stream idle between consecutive steps (event after step k's last launch to "
-                        "event before step k+1's first), 8 untraced steps after the timed region"}
+                        "event before step k+1's first), 8 untraced steps after the timed region; "
+                        "host_enqueue_ms is the host time of one step call, which includes the wait for the "
+                        "replay two steps back (the in-flight bound), so it equals the device step time once the "
+                        "host is ahead"}
 
     # roofline leg: one instrumented step, HIP events around every conv launch.
     # Two more (unsynchronised) steps are queued first so the host enqueues

@@ -139,10 +139,21 @@ __device__ __forceinline__ int ktile_off(int row, int slot) { return row * 128 +
 
 // WGRAD tiles: [BK m-rows][COLS elems], cols contiguous (as in HBM).
 template <typename T, int COLS> struct MTile;
+// 16-B chunk XOR of row `row` in a 64-column (128-B row) MTile: a transposed
+// fragment read (read_mfrag / read_tfrag) touches rows r0 + {0..3, 8..11} in
+// one 32-lane half, and two rows of equal parity share the 32 banks of one
+// 128-B half-line -- so the four equal-parity rows need four different 32-B
+// column groups for every r0.  Row bits 1 and 3 pick the group (the former
+// row & 3 selector repeated every 8 rows: rows r and r + 8 collided, a 2-way
+// conflict on every read, SQ_LDS_BANK_CONFLICT = 0.50 of the active LDS
+// cycles of conv_halo_wgrad_kernel).
+__device__ __forceinline__ int mt64_chunk_xor(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1; }
+
 template <int COLS> struct MTile<__bf16, COLS> {
   static constexpr int ROW_BYTES = COLS * 2;
   static constexpr int UNITS = COLS / 4;  // 8-byte units per row
   __device__ static __forceinline__ int swz(int row) {
+    if constexpr (COLS == 64) return mt64_chunk_xor(row) << 1;
     int h = (row & 3) | (((row >> 3) & 1) << 2);
     return (h * 4) & (UNITS - 1) & ~3;
   }
@@ -2156,7 +2167,7 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
       const int px = i * 8 + (lane >> 3);
       const int sr = px / Wp, sc = px - sr * Wp;
       const int pin = p0 - 1 + sr, win = sc - 1;
-      const int ch = (lane & 7) ^ ((px & 3) << 1);  // MTile<64>: 16-B chunk k at k ^ 2 (row & 3)
+      const int ch = (lane & 7) ^ mt64_chunk_xor(px);  // MTile<64>
       const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
       const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
       blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
@@ -2164,7 +2175,7 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
     for (int i = wave; i < HWG_DBUF / 1024; i += NW) {  // dy rows of the padded grid
       const int m = i * 8 + (lane >> 3);
       const int j = m / Wp, q = m - j * Wp;
-      const int ch = (lane & 7) ^ ((m & 3) << 1);
+      const int ch = (lane & 7) ^ mt64_chunk_xor(m);
       const bool ok = m < mrows && q < a.W;
       const uint32_t off = (uint32_t)(((((long)n * a.H + p0 + j) * a.W + q) * 64 + ch * 8) * 2);
       blds16(rsD, ok ? off : SSIP_OOB, Ds + i * 1024);
@@ -2177,13 +2188,31 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
 #pragma unroll
     for (int b = 0; b < 9; ++b) acc[x][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // column block b of this wave: tap t = (9 wn + b) / 4, channels 16 ((9 wn + b) % 4) ..
-  int toff[9], ccol[9];
+  // Per-lane LDS byte offsets of the transposed fragment reads at k-step 0
+  // (read_tfrag's rows r0 and r0 + 4): a k-step adds 32 rows = 4096 B and
+  // leaves row bits 1 and 3 -- the swizzle's -- unchanged.
+  int xo[9][2], dof[2][2];
+  {
+    const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
 #pragma unroll
-  for (int b = 0; b < 9; ++b) {
-    const int nb = 9 * wn + b, t = nb >> 2;
-    toff[b] = (t / 3) * Wp + (t % 3);
-    ccol[b] = (nb & 3) * 16;
+    for (int b = 0; b < 9; ++b) {
+      const int nb = 9 * wn + b, t = nb >> 2;
+      const int toff = (t / 3) * Wp + (t % 3), ccol = (nb & 3) * 16;
+      xo[b][0] = MTile<__bf16, 64>::off(toff + 8 * tg + tq, ccol + 4 * tp);
+      xo[b][1] = MTile<__bf16, 64>::off(toff + 8 * tg + tq + 4, ccol + 4 * tp);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      dof[x][0] = MTile<__bf16, 64>::off(8 * tg + tq, (2 * wm + x) * 16 + 4 * tp);
+      dof[x][1] = MTile<__bf16, 64>::off(8 * tg + tq + 4, (2 * wm + x) * 16 + 4 * tp);
+    }
   }
+  auto tfrag_at = [](Frag<T>& f, const char* a0, const char* a1) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
+    v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a0));
+    v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) v4bf*)(a1));
+    f.v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
 
   if (u0 < u1) issue(u0, smem, smem + HWG_XBUF);
   bool first = true;
@@ -2198,9 +2227,9 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
     Frag<T> fa[2][2], fb[2][9];
     auto load_step = [&](int ks, Frag<T>(&ra)[2], Frag<T>(&rb)[9]) {
 #pragma unroll
-      for (int x = 0; x < 2; ++x) read_tfrag(ra[x], Ds, 32 * ks, (2 * wm + x) * 16, lane);
+      for (int x = 0; x < 2; ++x) tfrag_at(ra[x], Ds + 4096 * ks + dof[x][0], Ds + 4096 * ks + dof[x][1]);
 #pragma unroll
-      for (int b = 0; b < 9; ++b) read_tfrag(rb[b], Xs, 32 * ks + toff[b], ccol[b], lane);
+      for (int b = 0; b < 9; ++b) tfrag_at(rb[b], Xs + 4096 * ks + xo[b][0], Xs + 4096 * ks + xo[b][1]);
     };
     load_step(0, fa[0], fb[0]);
 #pragma unroll
@@ -2275,7 +2304,7 @@ __global__ void __launch_bounds__(512, 2) conv_stem_wgrad_kernel(const StemWgArg
     for (int i = wave; i < SWG_DBUF / 1024; i += NW) {
       const int m = i * 8 + (lane >> 3);
       const int j = m / STEM_QP, q = m - j * STEM_QP;
-      const int ch = (lane & 7) ^ ((m & 3) << 1);  // MTile<64> swizzle
+      const int ch = (lane & 7) ^ mt64_chunk_xor(m);  // MTile<64> swizzle
       const bool ok = q < a.Q;
       const uint32_t off = (uint32_t)(((((long)n * a.P + p0 + j) * a.Q + q) * 64 + ch * 8) * 2);
       blds16(rsD, ok ? off : SSIP_OOB, Ds + i * 1024);
@@ -2538,7 +2567,7 @@ __global__ void __launch_bounds__(768, 1) conv_stem_bwd_wgrad2_kernel(const Stem
         const float d = (t > 0.f ? t : 0.f) > 0.f ? dz[px][e] : 0.f;
         o[e] = (__bf16)(ca[e] * d + cb[e] * yv + ck[e]);
       }
-      *reinterpret_cast<v4bf*>(D + r * 128 + (((c4 >> 1) ^ ((r & 3) << 1)) << 4) + (c4 & 1) * 8) = o;
+      *reinterpret_cast<v4bf*>(D + r * 128 + (((c4 >> 1) ^ mt64_chunk_xor(r)) << 4) + (c4 & 1) * 8) = o;
     }
   };
 

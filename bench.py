@@ -78,6 +78,10 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=None,
                     help="images per CPU-baseline step (default: the GPU batch; 16 for resnet50 at 512, where one "
                          "full 128-image CPU step takes minutes)")
+    ap.add_argument("--profile-leg", default=None, choices=["full", "production"],
+                    help="profiling run (no JSON line): warm-up, then --steps repetitions of that roofline leg "
+                         "alone, without event timers, for rocprofv3 --kernel-trace / --pmc "
+                         "(tools/roofline_from_trace.py takes the last complete step)")
     ap.add_argument("--max-inflight", type=int, default=None,
                     help="host waits for step k - N before enqueueing step k (0: never; default: SemiStep's own "
                          "bound on launch-plan replays, $SSIP_MAX_INFLIGHT or 2)")
@@ -221,6 +225,35 @@ def extract_bench(args):
     print(json.dumps(out))
 
 
+def roofline_leg(step, x_l, y_l, x_u, kind, ops, resnet_mod, timer=True):
+    """One step with every launch on one stream and (timer) HIP events around
+    every conv launch.  kind "full": the wgrads at their full-chip grids;
+    "production": with the side stream's grid budgets.  Two unsynchronised
+    steps are queued first so the host enqueues the eager instrumented step
+    while the device is still busy: each event bracket then holds its
+    kernel's execution, not device idle time waiting for the host's next
+    launch (the brackets agree with rocprofv3's kernel durations,
+    profiles/r5_roofline_leg_*.txt)."""
+    for _ in range(2):
+        step(x_l, y_l, x_u)
+    t = ops.ConvTimer() if timer else None
+    ops.set_conv_timer(t)
+    saved = (step.graph, step.plan, step.overlap, resnet_mod.WGRAD_SIDE_STREAM, resnet_mod.WGRAD_BUDGET_SERIAL)
+    # every launch on one stream: an event bracket must not include queueing
+    # behind a kernel of another stream (weak forward, side-stream wgrads)
+    step.graph, step.plan, step.overlap = False, False, False
+    resnet_mod.WGRAD_SIDE_STREAM = False
+    resnet_mod.WGRAD_BUDGET_SERIAL = kind == "production"
+    try:
+        step(x_l, y_l, x_u)
+    finally:
+        (step.graph, step.plan, step.overlap, resnet_mod.WGRAD_SIDE_STREAM,
+         resnet_mod.WGRAD_BUDGET_SERIAL) = saved
+        ops.set_conv_timer(None)
+    torch.cuda.synchronize()
+    return {"summary": t.summary(), "timer": t} if t is not None else None
+
+
 def main():
     args = parse()
     if args.workload == "extract":
@@ -268,6 +301,11 @@ def main():
 
     for _ in range(args.warmup):
         step(x_l, y_l, x_u)
+    if args.profile_leg:
+        for _ in range(args.steps):
+            roofline_leg(step, x_l, y_l, x_u, args.profile_leg, ops, resnet_mod, timer=False)
+        print(f"profile-leg {args.profile_leg}: {args.steps} legs done", file=sys.stderr)
+        return
     slots = step.input_slots()
     if slots is not None and os.environ.get("SSIP_NO_INPUT_SLOTS") != "1":
         # the synthetic batch written once into the buffers the recorded plan
@@ -319,30 +357,16 @@ def main():
                         "replay two steps back (the in-flight bound), so it equals the device step time once the "
                         "host is ahead"}
 
-    # roofline leg: one instrumented step, HIP events around every conv launch.
-    # Two more (unsynchronised) steps are queued first so the host enqueues
-    # the eager instrumented step while the device is still busy: each event
-    # bracket then holds its kernel's execution, not device idle time waiting
-    # for the host's next launch (the brackets agree with rocprofv3's kernel
-    # durations, profiles/r2_bench_family_summary.txt)
-    for _ in range(2):
-        step(x_l, y_l, x_u)
-    timer = ops.ConvTimer()
-    ops.set_conv_timer(timer)
-    # the same kernels launched one by one from Python, each bracketed by events
-    graph, step.graph = step.graph, False
-    plan_mode, step.plan = step.plan, False
-    # every launch on one stream: an event bracket must not include queueing
-    # behind a kernel of another stream (weak forward, side-stream wgrads)
-    side, resnet_mod.WGRAD_SIDE_STREAM = resnet_mod.WGRAD_SIDE_STREAM, False
-    overlap, step.overlap = step.overlap, False
-    step(x_l, y_l, x_u)
-    step.graph = graph
-    step.plan = plan_mode
-    step.overlap = overlap
-    resnet_mod.WGRAD_SIDE_STREAM = side
-    ops.set_conv_timer(None)
-    summ = timer.summary()
+    # roofline legs (one instrumented step each, bench_roofline_leg): "full" --
+    # the conv family's own rate, every launch at its full-chip grid -- is the
+    # line's `frac`; "production" keeps the side-stream wgrads' grid budgets
+    # (one workgroup per CU; half the CUs for the layer-1 wgrad) that the
+    # overlapped step actually runs, serialised, as `frac_production`
+    legs = {}
+    for kind in ("production", "full"):
+        legs[kind] = roofline_leg(step, x_l, y_l, x_u, kind, ops, resnet_mod)
+    summ = legs["full"]["summary"]
+    timer = legs["full"]["timer"]
     conv_flops = sum(v[0] for v in summ.values())
     conv_ms = sum(v[1] for v in summ.values())
     conv_launches = sum(v[2] for v in summ.values())
@@ -352,6 +376,11 @@ def main():
     # per-launch speed of light: max(FLOPs / MFMA peak, algorithmic bytes / HBM peak)
     # -- layer 1's 64-channel convs sit below the ridge point (~310 FLOP/B), HBM-bound
     sol_s, meas_s = timer.sol(peak * 1e12, HBM_PEAK_BPS)
+    psumm = legs["production"]["summary"]
+    prod_ms = sum(v[1] for v in psumm.values())
+    prod_achieved = sum(v[0] for v in psumm.values()) / (prod_ms * 1e-3) / 1e12
+    by_pass = {k: {"tflop": round(v[0] / 1e12, 4), "ms": round(v[1], 3), "launches": v[2],
+                   "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1)} for k, v in sorted(summ.items())}
 
     # HBM traffic of the same family from the committed rocprofv3 PMC passes of
     # THIS workload (tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE, separate
@@ -422,7 +451,16 @@ def main():
                          "kernel": "conv family: conv_glds / conv_halo / conv_stem_halo / conv_halo_wgrad / "
                                    "conv_stem_bwd_wgrad (fwd+dgrad+wgrad, incl. wgrad slab reduce), "
                                    f"{conv_launches} launches/step, {conv_flops / 1e12:.3f} TFLOP/step "
-                                   f"in {conv_ms:.3f} ms",
+                                   f"in {conv_ms:.3f} ms (single stream, every launch at its full-chip grid; "
+                                   "rocprofv3 of this leg: `python bench.py --profile-leg full`, "
+                                   "tools/roofline_from_trace.py)",
+                         "by_pass": by_pass,
+                         "frac_production": round(prod_achieved / peak, 4),
+                         "production": {"achieved": round(prod_achieved, 1), "ms": round(prod_ms, 3),
+                                        "note": "the same launches with the side-stream wgrads' grid budgets "
+                                                "the overlapped step runs (one workgroup per CU; half the CUs for "
+                                                "the layer-1 wgrad), still serialised on one stream: "
+                                                "`python bench.py --profile-leg production`"},
                          "sol": {"frac": round(sol_s / meas_s, 4), "sol_ms": round(sol_s * 1e3, 3),
                                  "algorithmic_bytes": conv_bytes, "hbm_peak_gbps": HBM_PEAK_BPS / 1e9,
                                  "note": "sum over the same launches of max(FLOPs / MFMA peak, algorithmic bytes / "

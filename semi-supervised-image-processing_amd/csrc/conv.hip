@@ -2858,7 +2858,9 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
 // the ones choose_glds() selects (round 3's wider tuning sets are on the
 // r3-variants branch, with tools/tune_conv.py's lists)
 #define SSIP_GLDS_FD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2) X(128, 128, 4, 4, 3)
-#define SSIP_GLDS_WG(X) X(128, 128, 4, 2, 2) X(64, 128, 2, 4, 2)
+#define SSIP_GLDS_WG(X)                                                                                     \
+  X(128, 128, 4, 2, 2) X(64, 128, 2, 4, 2) X(128, 128, 4, 2, 3) X(256, 128, 4, 2, 2) X(128, 256, 2, 4, 2)    \
+  X(256, 256, 4, 2, 2) X(256, 256, 4, 4, 2)
 #define SSIP_GLDS_POST(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2)
 #define SSIP_GLDS_FOLD(X) SSIP_GLDS_FD(X)
 #define SSIP_GLDS_STEM(X) X(128, 64, 4, 2, 2)

@@ -221,7 +221,9 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(const WprepTable
   for (int q = 0; q < 16; ++q) {
     const int k = k0 + ty + 4 * q;
     float v = vals[q];
-    if (e.kscale && k < e.K) v *= e.kscale[k];
+    // only in-range elements take the folded BN scale: a padding zero times a
+    // negative scale would store -0.0 where ssip_weight_prep stores +0.0
+    if (e.kscale && k < e.K && c0 + tx < e.C && s < e.S) v *= e.kscale[k];
     tile[ty + 4 * q][tx] = v;
   }
   __syncthreads();

@@ -37,6 +37,7 @@ from ssip.dist import shard_range  # noqa: E402
 from .training import distributed as D  # noqa: E402
 from ssip import SSIPResNet  # noqa: E402
 from ssip.augment import GpuTransform  # noqa: E402
+from ssip.host import pil_extraction_transform  # noqa: E402
 
 DEFAULT_DATA_DIR = Path("mri_dataset_brain_cancer_oc")
 DEFAULT_OUTPUT_ROOT = Path("outputs")
@@ -152,6 +153,9 @@ def load_model(device: torch.device, dtype: str = "fp32", weights: Optional[Path
     for p in model.parameters():
         p.requires_grad_(False)
     model.embedding_only = True
+    # --device cpu (BASELINE config 1, the reference's feature_extraction.py:
+    # 519-522,542): the same module tree evaluated with torch's CPU operators
+    model.host_execution = device.type == "cpu"
     return model.to(device)
 
 
@@ -172,6 +176,8 @@ def batched(items: Sequence, batch_size: int) -> Iterable[Sequence]:
 def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_size: int = BATCH_SIZE,
                        dtype: str = "fp32", weights: Optional[Path] = None,
                        decode_threads: int = 8, allow_random_init: bool = False) -> ExtractionResults:
+    if device.type == "cpu":
+        return _extract_embeddings_host(records, batch_size, weights, decode_threads, allow_random_init)
     model = load_model(device, dtype, weights, allow_random_init)
     tf = build_transform(model.compute_dtype)
     embeddings: List[np.ndarray] = []
@@ -230,6 +236,52 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
     embeddings = [torch.cat(embeddings).cpu().numpy()] if embeddings else []
     if D.world() > 1:
         embeddings, kept, failures, times = (D.gather_list(v) for v in (embeddings, kept, failures, times))
+    if not embeddings:
+        raise RuntimeError("No embeddings were generated; all images failed to decode?")
+    mat = np.concatenate(embeddings, 0)
+    logging.info("Computed embeddings with shape %s", mat.shape)
+    return ExtractionResults(mat, kept, failures, times, model.init_source)
+
+
+def _extract_embeddings_host(records: List[ImageRecord], batch_size: int, weights: Optional[Path],
+                             decode_threads: int, allow_random_init: bool) -> ExtractionResults:
+    """--device cpu: the reference's loop (decode + transform per file, a
+    stacked batch through the frozen backbone, fp32), with the per-file
+    decode + transform on a host thread pool (ssip/host.py)."""
+    model = load_model(torch.device("cpu"), "fp32", weights, allow_random_init)
+    embeddings: List[np.ndarray] = []
+    kept: List[ImageRecord] = []
+    failures: List[Path] = []
+    times: List[float] = []
+    logging.info("Beginning feature extraction over %d records (host)", len(records))
+
+    def load(rec):
+        try:
+            with Image.open(rec.absolute_path) as img:
+                return rec, pil_extraction_transform(img, TARGET_RESIZE, TARGET_CROP, IMAGENET_MEAN,
+                                                     IMAGENET_STD), None
+        except (UnidentifiedImageError, OSError) as exc:
+            return rec, None, exc
+
+    with ThreadPoolExecutor(max_workers=decode_threads) as pool:
+        for chunk in batched(records, batch_size):
+            t0 = time.perf_counter()
+            ok_recs, tensors = [], []
+            for rec, t, exc in pool.map(load, chunk):
+                if exc is not None:
+                    logging.error("Failed to decode %s: %s", rec.absolute_path, exc)
+                    failures.append(rec.absolute_path)
+                    continue
+                ok_recs.append(rec)
+                tensors.append(t)
+            if not tensors:
+                continue
+            with torch.no_grad():
+                feats = model(torch.stack(tensors)).flatten(1)
+            embeddings.append(feats.numpy())
+            kept.extend(ok_recs)
+            per = (time.perf_counter() - t0) / len(ok_recs)
+            times.extend([per] * len(ok_recs))
     if not embeddings:
         raise RuntimeError("No embeddings were generated; all images failed to decode?")
     mat = np.concatenate(embeddings, 0)
@@ -353,9 +405,13 @@ def main(argv=None) -> None:
     args = parse_args(argv)
     configure_logging(verbose=args.verbose)
     device = torch.device(args.device)
-    if device.type != "cuda":
-        raise RuntimeError("ssip feature extraction runs on the HIP device (--device cuda)")
-    device = D.setup(device)  # torchrun: one rank per GPU, file list sharded by batch
+    if device.type not in ("cuda", "cpu"):
+        raise RuntimeError(f"ssip feature extraction runs on the HIP device (--device cuda) or the host "
+                           f"(--device cpu), not {device}")
+    if device.type == "cuda":
+        device = D.setup(device)  # torchrun: one rank per GPU, file list sharded by batch
+    elif args.dtype != "fp32":
+        raise RuntimeError("--device cpu computes in fp32 (the reference's precision)")
     logging.info("Starting feature extraction on device %s", device)
     records = discover_image_records(args.data_dir)
     t0 = time.perf_counter()

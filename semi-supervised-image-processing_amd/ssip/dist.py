@@ -43,9 +43,17 @@ def init_from_env(backend: Optional[str] = None):
 
 
 class GradBucketer:
-    def __init__(self, arena, bucket_bytes: int = 16 << 20, group=None):
+    """``premul`` != 1 (RCCL only): each rank's bucket is multiplied by it
+    inside the all-reduce (ncclPreMulSum) and the AdamW grad scale divides it
+    back out.  With a power of two the result is bit-identical to premul 1;
+    tests use it so that a world-size-1 all-reduce is not an identity (a
+    bucket reduced before its gradients landed, or an AdamW launch that does
+    not wait for the reduction, then changes the weights)."""
+
+    def __init__(self, arena, bucket_bytes: int = 16 << 20, group=None, premul: float = 1.0):
         self.arena = arena
         self.group = group
+        self.premul = float(premul)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # collectives whenever a process group exists, also at world size 1
         # (RCCL then copies in place: the one-GPU RCCL test runs this path)
@@ -82,7 +90,15 @@ class GradBucketer:
         # comm stream behind the replay
         self.capture_mode = False
         self._comm = None
+        self._op = None
         self.reset()
+
+    def _reduce_op(self):
+        if self.premul == 1.0:
+            return dist.ReduceOp.SUM
+        if self._op is None:
+            self._op = dist._make_nccl_premul_sum(self.premul)
+        return self._op
 
     def reset(self):
         self.pending = [set(i for i in idxs if self.params[i].requires_grad) for idxs in self.buckets]
@@ -97,7 +113,7 @@ class GradBucketer:
             return
         lo, hi = self.ranges[b]
         if self.active:
-            self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+            self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=self._reduce_op(), group=self.group,
                                                 async_op=True))
 
     def end_capture(self) -> None:
@@ -115,7 +131,7 @@ class GradBucketer:
             if self.active and any(self.params[i].requires_grad for i in self.buckets[b]):
                 lo, hi = self.ranges[b]
                 with torch.cuda.stream(self._comm):
-                    self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM,
+                    self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=self._reduce_op(),
                                                         group=self.group, async_op=True))
         self.launched = [True] * len(self.buckets)
 
@@ -129,8 +145,13 @@ class GradBucketer:
             if not self.pending[b]:
                 self._launch(b)
 
+    def grad_scale(self) -> float:
+        """The factor AdamW applies to the reduced gradients: the 1/world
+        average, and the premultiplier divided back out."""
+        return 1.0 / (self.world * (self.premul if self.active else 1.0))
+
     def finish(self) -> float:
-        """Launch anything left, wait, and return the grad scale (1/world)."""
+        """Launch anything left, wait, and return the grad scale (1 / (world * premul))."""
         for b in range(len(self.buckets)):
             if any(self.params[i].requires_grad for i in self.buckets[b]):
                 self._launch(b)
@@ -139,7 +160,7 @@ class GradBucketer:
         self.handles = []
         if self._comm is not None:  # graph mode: the comm stream also carried the event waits
             torch.cuda.current_stream().wait_stream(self._comm)
-        return 1.0 / self.world
+        return self.grad_scale()
 
 
 def shard_range(n: int, rank: int, world: int):

@@ -29,6 +29,7 @@ class AdamW(torch.optim.Optimizer):
         self._runs_cache: Dict[int, List[Tuple[int, int, List[torch.Tensor]]]] = {}
         self._sched = None     # per group: fp64 device tensor {lr, t, lr/(1-b1^t), sqrt(1-b2^t), ...}
         self._sched_lr = None
+        self._sched_betas = None
         # data parallelism (src/training/distributed.attach_grad_allreduce): a
         # GradBucketer whose all-reduces step() waits for, averaging by 1/world
         self.dp_bucketer = None
@@ -50,7 +51,7 @@ class AdamW(torch.optim.Optimizer):
             return
         self._ensure_flat_state()
         dev = self.param_groups[0]["params"][0].device
-        self._sched, self._sched_lr = [], []
+        self._sched, self._sched_lr, self._sched_betas = [], [], []
         for group in self.param_groups:
             t = 0.0
             for p in group["params"]:
@@ -63,6 +64,7 @@ class AdamW(torch.optim.Optimizer):
             self._sched.append(torch.tensor([group["lr"], t, 0.0, 0.0, 0.0, 0.0, 0.0], dtype=torch.float64,
                                             device=dev))
             self._sched_lr.append(group["lr"])
+            self._sched_betas.append(tuple(group["betas"]))
 
     def _ensure_flat_state(self):
         if self.arena is not None and self._flat_state is None:
@@ -163,6 +165,13 @@ class AdamW(torch.optim.Optimizer):
         if group["lr"] != self._sched_lr[gi]:  # an LR scheduler moved it (host decision, eager only)
             sched[0].fill_(group["lr"])
             self._sched_lr[gi] = group["lr"]
+        if tuple(group["betas"]) != self._sched_betas[gi]:
+            # the advancing launch reads bias corrections the previous step
+            # staged with the old betas (slots 5-6): drop them, so it
+            # evaluates the corrections from this step's betas (torch reads
+            # the betas at every step)
+            sched[5:7].zero_()
+            self._sched_betas[gi] = tuple(group["betas"])
         for p in params:
             self._init_state(p)
         # the first update launch of the step advances the schedule itself

@@ -221,6 +221,9 @@ class SSIPResNet(nn.Module):
         self._bn_epoch = 0
         self._arena = None
         self.embedding_only = False
+        # the CPU device was asked for (src.feature_extraction --device cpu):
+        # a CPU model's eval forward runs ssip/host.py instead of raising
+        self.host_execution = False
         # backward tail (single process, SemiStep): leave the stem wgrad (the
         # last kernel of the backward, on the wgrad side stream) unjoined; the
         # main stream only waits for the wgrads before it, so the optimizer
@@ -307,6 +310,12 @@ class SSIPResNet(nn.Module):
         else:
             dev = self.conv1.weight.device
             if dev.type != "cuda":
+                if self.host_execution:
+                    # the frozen eval pass on the CPU, asked for explicitly
+                    # (feature extraction --device cpu): ssip/host.py
+                    from .host import host_forward
+
+                    return host_forward(self, x)
                 raise RuntimeError("SSIPResNet runs on the HIP device only; call model.to('cuda') first")
             x = x.to(dev, non_blocking=True)
             if x.dim() != 4 or x.shape[1] != 3:
@@ -630,6 +639,9 @@ def _grad_target(p: torch.Tensor, arena) -> Tuple[torch.Tensor, bool]:
 # latency-bound BN-backward passes and finalize launches overlap with them.
 # WGRAD_SIDE_STREAM = False serialises everything on the current stream.
 WGRAD_SIDE_STREAM = os.environ.get("SSIP_WGRAD_STREAM", "1") != "0"
+# measurement only (bench.py's production roofline leg): keep the side
+# stream's wgrad grid budgets when everything runs serialised on one stream
+WGRAD_BUDGET_SERIAL = False
 _side_streams = {}
 
 
@@ -840,7 +852,8 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             return
         tgt, acc = _grad_target(w, arena)
         if side is None:
-            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace)
+            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
+                           max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev) if WGRAD_BUDGET_SERIAL else 0)
             return
         ops.wait_stream(side, main)
         with torch.cuda.stream(side):

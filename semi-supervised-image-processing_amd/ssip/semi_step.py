@@ -324,7 +324,7 @@ class SemiStep:
         if self._plan is None:
             self._static = (x_l.clone(), y_l.clone(), x_u.clone()) + self._dev_params(params, dev)
             plan = Plan()
-            scale = 1.0 / self.bucketer.world if self.bucketer is not None else 1.0
+            scale = self.bucketer.grad_scale() if self.bucketer is not None else 1.0
             with plan:
                 out = self._fwd_bwd(*self._static)
                 if self.bucketer is not None:

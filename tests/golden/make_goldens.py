@@ -146,8 +146,12 @@ def main() -> None:
         def __getitem__(self, i):
             return self.x[i], int(self.y[i])
 
+    rec6 = _PredRecorder()
+    real_metric = C.compute_accuracy_f1
+    C.compute_accuracy_f1 = rec6.wrap_metric(real_metric)
     torch.manual_seed(42)
     m2 = C.create_model(2, pretrained=False)
+    m2.register_forward_hook(rec6.hook)
     tr_ds, va_ds = Tiny(24, 1), Tiny(8, 2)
     sampler = C.make_balanced_sampler(tr_ds.y.tolist())
     tl = DataLoader(tr_ds, batch_size=8, sampler=sampler, num_workers=0)
@@ -160,11 +164,13 @@ def main() -> None:
                                  num_epochs=3, early_stopping_patience=3, model_path=ck)
         saved = torch.load(ck, weights_only=True)
         same = all(torch.equal(saved[k], v) for k, v in m2.state_dict().items())
+    C.compute_accuracy_f1 = real_metric
     m2.eval()
     with torch.no_grad():
         final_logits = m2(va_ds.x).numpy()
     goldens["train_model"] = {"history": hist, "final_eval_logits": final_logits.tolist(),
-                              "checkpoint_equals_returned": bool(same), "epochs": 3, "batch_size": 8}
+                              "checkpoint_equals_returned": bool(same), "epochs": 3, "batch_size": 8,
+                              "metric_calls": rec6.metric_calls}
 
     # 7. generate_pseudo_labels on fixed logits (identity "model" over a tiny loader)
     class LogitModel(torch.nn.Module):
@@ -264,8 +270,14 @@ def _pipelines(C, SS) -> dict:
             picks.extend([Path(p).name, int(l), float(c)] for p, l, c in out)
             return out
 
+        real_fns = {(mod, nm): getattr(mod, nm) for mod in (C, SS, SV)
+                    for nm in ("create_model", "compute_accuracy_f1", "evaluate_model") if hasattr(mod, nm)}
         try:
             for kind in ("semi", "supervised"):
+                rec = _PredRecorder()
+                for (mod, nm), fn in real_fns.items():
+                    setattr(mod, nm, {"create_model": rec.wrap_create, "compute_accuracy_f1": rec.wrap_metric,
+                                      "evaluate_model": rec.wrap_eval}[nm](fn))
                 (td / kind).mkdir()
                 os.chdir(td / kind)
                 cfg = C.TrainingConfig(strong_data_dir=data / "avec_labels", weak_data_dir=data / "sans_label",
@@ -281,13 +293,68 @@ def _pipelines(C, SS) -> dict:
                     if "training_time_sec" in m:
                         m["training_time_sec"] = None
                 res[kind] = {"metrics": json.loads(json.dumps(metrics, default=float)),
-                             "artifacts": _read_artifacts(td / kind / "outputs", kind == "semi")}
+                             "artifacts": _read_artifacts(td / kind / "outputs", kind == "semi"),
+                             "metric_calls": rec.metric_calls, "eval_calls": rec.eval_calls}
+                for (mod, nm), fn in real_fns.items():
+                    setattr(mod, nm, fn)
             res["semi"]["pseudo_labels"] = picks
         finally:
+            for (mod, nm), fn in real_fns.items():
+                setattr(mod, nm, fn)
             os.chdir(cwd)
             os.environ.pop("SSIP_RESNET18_WEIGHTS", None)
             SS.generate_pseudo_labels = real
     return res
+
+
+class _PredRecorder:
+    """Per-sample predictions of the reference run, for prediction-level
+    parity: every compute_accuracy_f1 call (the history's
+    train_* / val_* values) with the P(class 1) of each of its samples -- the
+    softmax of the logits the calling loop took its argmax from, captured by
+    a forward hook on every model create_model returns (the last len(y_pred)
+    outputs before the call) -- and every evaluate_model call with its
+    threshold and per-sample probabilities."""
+
+    def __init__(self):
+        self.outs = []
+        self.metric_calls = []
+        self.eval_calls = []
+
+    def hook(self, _m, _inp, out):
+        self.outs.append(out.detach().float().cpu())
+
+    def wrap_create(self, create):
+        def create_model(*a, **k):
+            m = create(*a, **k)
+            m.register_forward_hook(self.hook)
+            return m
+        return create_model
+
+    def wrap_metric(self, real):
+        import torch
+
+        def compute_accuracy_f1(y_true, y_pred):
+            n = len(y_pred)
+            z = torch.cat(self.outs)[-n:] if n else torch.zeros(0, 2)
+            self.outs = []
+            p1 = torch.softmax(z, 1)[:, 1]
+            assert z.argmax(1).tolist() == list(map(int, y_pred)), "hooked logits do not match the predictions"
+            self.metric_calls.append({"y_true": list(map(int, y_true)), "y_pred": list(map(int, y_pred)),
+                                      "p1": [float(v) for v in p1]})
+            return real(y_true, y_pred)
+        return compute_accuracy_f1
+
+    def wrap_eval(self, real):
+        def evaluate_model(model, loader, device, pos_index=None, threshold=None):
+            out = real(model, loader, device, pos_index=pos_index, threshold=threshold)
+            _, yt, yp, pr, _ = out
+            self.outs = []
+            self.eval_calls.append({"threshold": threshold, "pos_index": pos_index,
+                                    "y_true": [int(v) for v in yt], "y_pred": [int(v) for v in yp],
+                                    "y_prob": [float(v) for v in pr]})
+            return out
+        return evaluate_model
 
 
 class _Recorder:

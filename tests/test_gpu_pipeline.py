@@ -4,10 +4,14 @@ of the three CLIs on a small synthetic on-disk dataset.
 
 Tolerances: fp32 path, logits/embeddings rel-max 1e-4; train_model history
 losses rel-max 2e-3 over 3 epochs of AdamW, final logits 2e-2 (see the
-comment in the test), accuracy and F1 (history train_f1 / val_f1, and precision / recall / f1 /
-rates of the results tables) within ONE flipped prediction of the reference
-run, checked jointly from the golden's own confusion matrix (test helpers
-below)."""
+comment in the test).  Accuracy and F1 (history train_* / val_*, the results
+tables) are pinned at the PREDICTION level (north_star: val accuracy/F1
+within +-0.5 pt of the reference run, i.e. the same predictions on these
+tiny sets): every sample's prediction must equal the reference run's, except
+a sample whose reference probability lies within the run's probability
+bound of the decision point (|p_ref - 0.5| for argmax, |p_ref - thr| for a
+threshold; the goldens record the reference's per-sample P, make_goldens.py
+_PredRecorder).  The aggregate one-flip checks stay as a second guard."""
 import json
 from pathlib import Path
 
@@ -87,6 +91,54 @@ def _acc_f1(acc, p, r, f1):
     return (acc, f1)
 
 
+def assert_preds_near_ties(y_true, y_pred, gold, bound, what, thr=None, thr_ref=None):
+    """Our per-sample predictions vs the reference run's (`gold`: y_true /
+    y_pred and p1 or y_prob).  Labels must be identical; a prediction may
+    differ only where the reference probability is within `bound` of the
+    decision point (0.5 for argmax; the threshold, widened by how far our
+    threshold moved from the reference's)."""
+    assert list(map(int, y_true)) == gold["y_true"], (what, "labels differ")
+    p = np.asarray(gold.get("p1", gold.get("y_prob")), np.float64)
+    if thr is None:
+        near = np.abs(p - 0.5) < bound
+    else:
+        near = np.abs(p - thr_ref) < bound + abs(float(thr) - float(thr_ref))
+    diff = np.asarray(list(map(int, y_pred))) != np.asarray(gold["y_pred"])
+    bad = np.nonzero(diff & ~near)[0]
+    assert bad.size == 0, (what, "prediction differs from the reference run away from a near-tie",
+                           [(int(i), gold["y_pred"][i], int(y_pred[i]), float(p[i])) for i in bad], bound)
+    return int(diff.sum())
+
+
+class _EvalSpy:
+    """Records every evaluate_model call (threshold, y_true, y_pred) of the
+    drop-in pipelines, in call order."""
+
+    def __init__(self, monkeypatch):
+        from src.training import common as C
+        from src.training import semi_supervised as SS
+        from src.training import supervised as SV
+
+        self.calls = []
+        real = C.evaluate_model
+
+        def spy(model, loader, device, pos_index=None, threshold=None):
+            out = real(model, loader, device, pos_index=pos_index, threshold=threshold)
+            self.calls.append((threshold, [int(v) for v in out[1]], [int(v) for v in out[2]]))
+            return out
+
+        for mod in (C, SS, SV):
+            monkeypatch.setattr(mod, "evaluate_model", spy)
+
+    def check(self, gold_calls, bound, what):
+        assert len(self.calls) == len(gold_calls), (what, len(self.calls), len(gold_calls))
+        flips = 0
+        for i, ((thr, yt, yp), g) in enumerate(zip(self.calls, gold_calls)):
+            assert (thr is None) == (g["threshold"] is None), (what, i)
+            flips += assert_preds_near_ties(yt, yp, g, bound, (what, "eval", i), thr, g["threshold"])
+        return flips
+
+
 class _MetricSpy:
     """Records the (y_true, y_pred) of every compute_accuracy_f1 call (the
     history's train_* and val_* entries, in call order)."""
@@ -103,14 +155,18 @@ class _MetricSpy:
 
         monkeypatch.setattr(C, "compute_accuracy_f1", spy)
 
-    def check_history(self, hist, gold_hist, call0, what):
+    def check_history(self, hist, gold_hist, call0, what, gold_calls=None, bound=None):
         """hist / gold_hist: one stage's history; the stage's epochs are calls
-        call0, call0 + 1, ... as (train, val) pairs.  Returns the next call index."""
+        call0, call0 + 1, ... as (train, val) pairs.  gold_calls: the
+        reference run's per-sample records of the same calls (prediction-level
+        check with `bound`).  Returns the next call index."""
         n_ep = len(gold_hist["train_acc"])
         assert len(hist["train_acc"]) == n_ep, what
         for e in range(n_ep):
             for j, split in enumerate(("train", "val")):
-                yt, _ = self.calls[call0 + 2 * e + j]
+                yt, yp = self.calls[call0 + 2 * e + j]
+                if gold_calls is not None:
+                    assert_preds_near_ties(yt, yp, gold_calls[call0 + 2 * e + j], bound, (what, split, e))
                 n_pos = sum(1 for y in yt if y == 1)  # F1 of class index 1 (pos_label=1), as the reference
                 ours = (hist[f"{split}_acc"][e], hist[f"{split}_f1"][e])
                 gold = (gold_hist[f"{split}_acc"][e], gold_hist[f"{split}_f1"][e])
@@ -170,11 +226,14 @@ def test_train_model_trajectory_matches_reference(dev, tmp_path, monkeypatch):
                             early_stopping_patience=3, model_path=ck)
     for k in ("train_loss", "val_loss"):
         assert _rel(hist[k], gold["history"][k]) < 2e-3, (k, hist[k], gold["history"][k])
-    # accuracy/F1: an untrained net on noise inputs has near-tied logits; a
-    # prediction may flip when |z1 - z0| is within the fp32 trajectory error,
-    # so allow at most one flipped prediction per epoch and split, jointly for
-    # accuracy and F1 (8 val / 24 train images)
-    assert spy.check_history(hist, gold["history"], 0, "train_model") == len(spy.calls)
+    # accuracy/F1 at the prediction level: an untrained net on noise inputs has
+    # near-tied logits, and this run's logits agree to 2e-2 of their scale
+    # (below), so |d(z1 - z0)| <= 2 * 2e-2 * max|z| and |dP| <= a quarter of
+    # that: a prediction may differ only where the reference's P(class 1) is
+    # that close to 0.5 (gold["metric_calls"]: the reference's per-sample P)
+    ref = np.asarray(gold["final_eval_logits"])
+    pbound = 2 * 2e-2 * np.abs(ref).max() / 4
+    assert spy.check_history(hist, gold["history"], 0, "train_model", gold["metric_calls"], pbound) == len(spy.calls)
     saved = torch.load(ck, weights_only=True)
     same = all(torch.equal(saved[k].cpu(), v.cpu()) for k, v in m.state_dict().items())
     assert same == gold["checkpoint_equals_returned"]  # the best_state alias quirk
@@ -185,7 +244,6 @@ def test_train_model_trajectory_matches_reference(dev, tmp_path, monkeypatch):
     # that are ~0 take a sign from rounding noise, so 9 steps diverge the
     # weights by O(lr) in those coordinates -> logits agree to ~1e-2, not 1e-5
     assert _rel(logits, gold["final_eval_logits"]) < 2e-2
-    ref = np.asarray(gold["final_eval_logits"])
     margin = np.abs(ref[:, 1] - ref[:, 0])
     # within the 2e-2 logit bound above, a margin under 2 x 2e-2 may flip
     safe = margin > 4e-2 * np.abs(ref).max()
@@ -298,6 +356,7 @@ def test_pipelines_match_reference_run(dev, tmp_path, monkeypatch, kind):
 
     gold = GOLD["pipeline"]
     mspy = _MetricSpy(monkeypatch)
+    espy = _EvalSpy(monkeypatch)
     data = tiny_dataset.make(tmp_path / "mri")
     w = tmp_path / "w.pt"
     torch.save(tiny_dataset.pretrained_state_dict(gold["weights_seed"]), w)
@@ -325,6 +384,14 @@ def test_pipelines_match_reference_run(dev, tmp_path, monkeypatch, kind):
     art = _read_artifacts(tmp_path / kind / "outputs", kind == "semi")
     ref = gold[kind]["artifacts"]
     assert art["files"] == ref["files"]
+    # prediction level (the run's probability bound, as the triage check below):
+    # every evaluate_model call -- test argmax, val, test at the operating
+    # threshold -- and every history metric call
+    PB = 2e-3
+    espy.check(gold[kind]["eval_calls"], PB, kind)
+    assert len(mspy.calls) == len(gold[kind]["metric_calls"])
+    for i, ((yt, yp), g) in enumerate(zip(mspy.calls, gold[kind]["metric_calls"])):
+        assert_preds_near_ties(yt, yp, g, PB, (kind, "history call", i))
     n_test = 4  # 20 % of 20 labelled images
     counts = ("TP", "FP", "TN", "FN")
     prf_cols = ("accuracy", "precision", "recall", "f1")

@@ -5,12 +5,18 @@ world size 1: the bucketer still issues every bucket's all-reduce through
 RCCL (ssip.dist.GradBucketer is active whenever a process group exists) --
 from the backward's grad-ready hooks (eager), from the launch plan's host
 callbacks during a C++ replay (plan), and on the comm stream behind a
-hipGraph replay (graph) -- and waits for them before AdamW.  An RCCL
-all-reduce over one rank is an in-place identity, so after the steps the
-weights must equal a run without any process group, bit for bit: a bucket
-reduced before its gradients were complete, or AdamW run before a bucket's
-completion, would differ.  The multi-GPU node runs the same code with world
-size > 1 (bench.py under torch.distributed.run).
+hipGraph replay (graph) -- and waits for them before AdamW.  A plain SUM
+over one rank is an in-place identity, so the buckets are reduced with
+ncclPreMulSum(2) and AdamW divides the 2 back out (GradBucketer(premul=2),
+grad_scale 0.5): exact in fp32, so after the steps the weights must equal a
+run without any process group bit for bit, while a bucket reduced before its
+gradients landed (they are then overwritten undoubled and halved) or an
+AdamW launch that does not wait for the reduction (it halves the undoubled
+gradients) changes them.  The negative control proves the test bites: a
+bucketer that all-reduces every bucket at the first grad-ready hook, before
+the wgrads that fill them were enqueued, must NOT reproduce the weights.
+The multi-GPU node runs the same code with world size > 1 (bench.py under
+torch.distributed.run).
 """
 import os
 
@@ -25,14 +31,22 @@ pytestmark = pytest.mark.gpu
 MODES = ("eager", "plan", "graph")
 
 
-def _make(dev, mode, with_bucketer):
+def _make(dev, mode, with_bucketer, early=False):
     from ssip import SSIPResNet, replace_fc
     from ssip.dist import GradBucketer
     from ssip.semi_step import SemiStep
 
+    class EarlyBucketer(GradBucketer):
+        """Negative control: every bucket is launched at the first hook."""
+
+        def mark_ready(self, params):
+            for b in range(len(self.buckets)):
+                self._launch(b)
+
     torch.manual_seed(0)
     m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2).to(dev).train()
-    bucketer = GradBucketer(m.flatten_parameters(), bucket_bytes=8 << 20) if with_bucketer else None
+    cls = EarlyBucketer if early else GradBucketer
+    bucketer = cls(m.flatten_parameters(), bucket_bytes=8 << 20, premul=2.0) if with_bucketer else None
     step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=64, bucketer=bucketer, seed=0,
                     plan=mode == "plan", graph=mode == "graph")
     step.opt.use_device_schedule()
@@ -65,8 +79,10 @@ def _worker(port, out):
         for mode in MODES:
             step = _make(dev, mode, True)
             assert step.bucketer.active and len(step.bucketer.buckets) > 1
+            assert step.bucketer.grad_scale() == 0.5
             res[mode] = _run_steps(step, dev)
             del step
+        res["early"] = _run_steps(_make(dev, "eager", True, early=True), dev)
         # the rank-0 broadcast the pipelines use for weights, over RCCL
         t = torch.arange(1 << 16, dtype=torch.float32, device=dev)
         dist.broadcast(t, 0)
@@ -90,3 +106,6 @@ def test_semi_step_rccl_world1_equals_single(dev, tmp_path):
     for mode in MODES:
         want = _run_steps(_make(dev, mode, False), dev)
         assert torch.equal(r[mode], want), mode
+        if mode == "eager":
+            # the control: all-reduced before the wgrads landed -> different weights
+            assert not torch.equal(r["early"], want)

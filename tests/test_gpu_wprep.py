@@ -17,13 +17,17 @@ SHAPES = [(64, 3, 7, 7, 4, 8), (64, 64, 3, 3, 64, 3), (128, 64, 3, 3, 64, 3), (1
           (256, 128, 3, 3, 128, 3), (512, 512, 3, 3, 512, 3), (2048, 512, 1, 1, 512, 1), (100, 70, 3, 3, 70, 3)]
 
 
-@pytest.mark.parametrize("scaled", [False, True])
+@pytest.mark.parametrize("scaled", [False, True, "negative"])
 def test_weight_prep_batch_matches_single(dev, scaled):
+    """"negative": scales of both signs (a folded BN with gamma < 0) -- the
+    channel / tap padding must stay +0.0, as the elementwise kernel stores it."""
     g = torch.Generator().manual_seed(7)
     items, want = [], []
     for (K, C, R, S, Cp, Sp) in SHAPES:
         w = torch.randn(K, C, R, S, generator=g).to(dev)
         ks = (torch.rand(K, generator=g) + 0.5).to(dev) if scaled else None
+        if scaled == "negative":
+            ks = ks * torch.where(torch.arange(K, device=dev) % 2 == 0, -1.0, 1.0)
         krsc = torch.full((K, R, Sp, Cp), float("nan"), device=dev, dtype=DT)
         crsk = torch.full((Cp, R, Sp, K), float("nan"), device=dev, dtype=DT)
         items.append((w, Cp, Sp, krsc, crsk, ks))

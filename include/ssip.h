@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 11
+#define SSIP_ABI_VERSION 12
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -131,13 +131,20 @@ int64_t ssip_conv_wgrad_workspace_bytes(const ssip_conv_desc* d);
 int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs, int c_real,
                     int s_real, int accumulate, void* workspace, int64_t workspace_bytes, void* stream);
 /* The same with a workgroup budget for the split-K grid of the LDS-DMA wgrad
- * (ABI 10): split count = ceil(max_workgroups / output tiles), for a wgrad
- * that shares the chip with another stream's kernels (the backward's side
- * stream beside the dgrad / BN-backward chain: one workgroup per CU leaves
- * each CU room for the main stream); 0 = ssip_conv_wgrad's full-chip grid.
- * The persistent layer-1 and stem wgrads (one workgroup per CU, all of its
- * LDS) run on at most max_workgroups CUs.  Same result up to the fp32 order
- * of the split / slab sum (fixed for a budget). */
+ * (ABI 10), for a wgrad that shares the chip with another stream's kernels
+ * (the backward's side stream beside the dgrad / BN-backward chain); 0 =
+ * ssip_conv_wgrad's full-chip grid.  ABI 12: with a budget the bf16 wgrad
+ * takes 16-wave 256x256 (K % 256 == 0) or 128x256 tiles that fit one
+ * workgroup per CU, and at most max_workgroups of them (split count =
+ * floor(max_workgroups / output tiles)); other tiles keep ceil(max_workgroups
+ * / tiles) splits ($SSIP_WGRAD_BIG=0: the full-grid tiles).  The persistent
+ * layer-1 and stem wgrads (one workgroup per CU, all of its LDS) run on at
+ * most max_workgroups CUs.  Same result up to the fp32 order of the split /
+ * slab sum (fixed for a budget).  The workspace a budget needs:
+ * ssip_conv_wgrad_workspace_bytes_budget (ABI 12; budget 0 =
+ * ssip_conv_wgrad_workspace_bytes) -- a budget may need more slab bytes than
+ * the full-grid plan. */
+int64_t ssip_conv_wgrad_workspace_bytes_budget(const ssip_conv_desc* d, int max_workgroups);
 int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs,
                            int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
                            int max_workgroups, void* stream);
@@ -147,6 +154,10 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
  * "halo<dgrad,TR=4,G=256>": lets tests assert that a shape exercises the
  * production kernel the benchmark runs. */
 int ssip_conv_kernel_name(int mode, const ssip_conv_desc* d, int dtype, char* buf, int buflen);
+/* ABI 12: the kernel ssip_conv_wgrad_budget selects with that budget (mode 2;
+ * fwd / dgrad ignore the budget) */
+int ssip_conv_kernel_name_budget(int mode, const ssip_conv_desc* d, int dtype, int max_workgroups, char* buf,
+                                 int buflen);
 
 /* ------------------------------------------------------------------------
  * BatchNorm2d (train / eval) fused with ReLU and the residual add.

@@ -110,22 +110,80 @@ def semi_step_reference(model, opt, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.
 
 
 class CpuSemiStep:
+    """The CPU step.  Views are made the way the reference's loaders make them:
+    on `workers` background workers (TrainingConfig.num_workers = 2,
+    common.py:54, 256-292), one step ahead of the model compute -- the
+    parameters are drawn in order on the calling thread (deterministic), the
+    Pillow work runs in a thread pool (Pillow releases the GIL) while the
+    previous step computes.  workers=0: views made synchronously."""
+
     def __init__(self, seed: int = 42, tau: float = 0.7, lambda_u: float = 1.0, size: int = 224,
-                 arch: str = "resnet18"):
+                 arch: str = "resnet18", workers: int = 2):
         torch.manual_seed(seed)
         self.model = getattr(tvm, arch)()
         self.model.fc = torch.nn.Linear(self.model.fc.in_features, 2)
         self.opt = torch.optim.AdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-4)
         self.tau, self.lambda_u, self.size = tau, lambda_u, size
         self.g = torch.Generator().manual_seed(seed)
+        self.workers = workers
+        self._pool = None
+        self._next = None
+
+    def _draw(self, n: int, degrees: float, strong: bool):
+        out = []
+        for _ in range(n):
+            flip = bool(torch.rand(1, generator=self.g) < 0.5)
+            ang = float(torch.empty(1).uniform_(-degrees, degrees, generator=self.g).item())
+            extra = None
+            if strong:
+                u = torch.rand(4, generator=self.g)
+                side = int(0.25 * self.size)
+                x0 = int(float(u[2]) * (self.size - side))
+                y0 = int(float(u[3]) * (self.size - side))
+                extra = (1.0 + 0.4 * (2 * float(u[0]) - 1), 1.0 + 0.4 * (2 * float(u[1]) - 1),
+                         (x0, y0, x0 + side, y0 + side))
+            out.append((flip, ang) + (extra if extra is not None else (1.0, 1.0, None)))
+        return out
+
+    def _views(self, x_l: np.ndarray, x_u: np.ndarray):
+        S = self.size
+        dl, dw, ds = self._draw(len(x_l), 10.0, False), self._draw(len(x_u), 10.0, False), \
+            self._draw(len(x_u), 30.0, True)
+        jobs = [(a, d) for a, d in zip(x_l, dl)] + [(a, d) for a, d in zip(x_u, dw)] + \
+               [(a, d) for a, d in zip(x_u, ds)]
+
+        def make(job):
+            a, d = job
+            return view_from_draw(Image.fromarray(a), S, *d)
+
+        def run():
+            if self._pool is None:
+                return [make(j) for j in jobs]
+            # the workers split the step's views (a DataLoader worker builds whole batches)
+            k = -(-len(jobs) // self.workers)
+            parts = [self._pool.submit(lambda js=jobs[i:i + k]: [make(j) for j in js])
+                     for i in range(0, len(jobs), k)]
+            return [v for p in parts for v in p.result()]
+
+        def stack():
+            v = run()
+            nl, nu = len(x_l), len(x_u)
+            return torch.stack(v[:nl]), torch.stack(v[nl:nl + nu]), torch.stack(v[nl + nu:])
+
+        return stack
 
     def __call__(self, x_l: np.ndarray, y_l: torch.Tensor, x_u: np.ndarray) -> float:
-        S = self.size
-        il = [Image.fromarray(a) for a in x_l]
-        iu = [Image.fromarray(a) for a in x_u]
-        xl = torch.stack([_view(i, S, 10.0, False, self.g) for i in il])
-        xw = torch.stack([_view(i, S, 10.0, False, self.g) for i in iu])
-        xs = torch.stack([_view(i, S, 30.0, True, self.g) for i in iu])
+        from concurrent.futures import ThreadPoolExecutor
+
+        if self.workers > 0 and self._pool is None:
+            self._pool = ThreadPoolExecutor(self.workers + 1)
+        if self._next is None:
+            cur = self._views(x_l, x_u)()
+        else:
+            cur = self._next.result()
+        if self._pool is not None:  # the next step's views while this one computes
+            self._next = self._pool.submit(self._views(x_l, x_u))
+        xl, xw, xs = cur
         m = self.model
         m.train()
         with torch.no_grad():
@@ -146,11 +204,20 @@ class CpuSemiStep:
             F.cross_entropy(z[Bl:], pseudo, reduction="none") * mask).mean()
         loss.backward()
         self.opt.step()
-        return float(loss)
+        return float(loss.detach())
+
+    def close(self):
+        if self._next is not None:
+            self._next.result()
+            self._next = None
+        if self._pool is not None:
+            self._pool.shutdown()
+            self._pool = None
 
 
 def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2, threads: int = 16,
-                  seed: int = 0, arch: str = "resnet18", size: int = 224, budget_s: float = 0.0) -> Dict:
+                  seed: int = 0, arch: str = "resnet18", size: int = 224, budget_s: float = 0.0,
+                  workers: int = 2) -> Dict:
     """Images/sec of the CPU step (warm-up steps, then
     the MEDIAN of the timed steps) on a bounded sample of steps x (Bl + Bu)
     images of the workload's own architecture and image size.  budget_s > 0
@@ -163,7 +230,7 @@ def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2,
     x_l = rng.integers(0, 256, (Bl, size, size, 3), dtype=np.uint8)
     x_u = rng.integers(0, 256, (Bu, size, size, 3), dtype=np.uint8)
     y_l = torch.from_numpy(rng.integers(0, 2, Bl))
-    step = CpuSemiStep(arch=arch, size=size)
+    step = CpuSemiStep(arch=arch, size=size, workers=workers)
     for i in range(warmup):
         t0 = time.perf_counter()
         step(x_l, y_l, x_u)
@@ -177,9 +244,11 @@ def time_cpu_step(Bl: int = 128, Bu: int = 128, steps: int = 5, warmup: int = 2,
         print(f"cpu_baseline step {i + 1}/{steps}: {times[-1]:.2f} s", file=sys.stderr, flush=True)
         if budget_s > 0 and len(times) >= 3 and sum(times) >= budget_s:
             break
+    step.close()
     dt = statistics.median(times)
     return {"value": (Bl + Bu) / dt, "step_s": dt, "threads": torch.get_num_threads(), "step_times_s": times,
             "steps_timed": len(times), "warmup": warmup,
             "sample": f"median of {len(times)} timed steps after {warmup} warm-up, each {Bl} labelled + {Bu} "
-                      f"unlabelled {size}x{size} uint8 images: PIL weak/strong views + torch fp32 {arch} weak "
+                      f"unlabelled {size}x{size} uint8 images: PIL weak/strong views (on {workers} background "
+                      f"workers one step ahead, as the reference's num_workers=2 loaders) + torch fp32 {arch} weak "
                       f"forward + joint fwd/bwd + AdamW (oracle/step_oracle.py)"}

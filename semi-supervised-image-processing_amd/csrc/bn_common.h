@@ -15,7 +15,8 @@ namespace {
 // channel whose records would take more than FIN_PT per thread is split over
 // S workgroups (fin_splits); their fp64 partial results go to a scratch area
 // behind the records (fin_scratch) and a one-wave-per-channel merge finishes
-// them.  SSIP_FIN_NT=64: one-wave workgroups without LDS (measured slower).
+// them.  (Round 3 measured one-wave finalize workgroups without LDS slower;
+// that variant and its SSIP_FIN_NT knob are gone.)
 // sums of up to three values over a 256-thread workgroup in fp64 with one
 // LDS round (wave butterflies, then the 4 wave totals in fixed order)
 template <int V>

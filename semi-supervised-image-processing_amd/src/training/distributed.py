@@ -81,8 +81,14 @@ def shard_loader(loader: DataLoader, even: bool = False) -> DataLoader:
     total = -(-nb // w) * w if nb > 0 else 0
     blo, bhi = shard_range(total, rank(), w)
     batches = [list(range((b % nb) * bs, min((b % nb + 1) * bs, n))) for b in range(blo, bhi)]
-    return DataLoader(ds, batch_sampler=batches, num_workers=loader.num_workers, pin_memory=loader.pin_memory,
-                      collate_fn=loader.collate_fn)
+    out = DataLoader(ds, batch_sampler=batches, num_workers=loader.num_workers, pin_memory=loader.pin_memory,
+                     collate_fn=loader.collate_fn)
+    # which of this rank's batches are wrap-around repeats: they run as steps
+    # (the gradient all-reduce needs every rank) but a caller keeps them out of
+    # the epoch's loss / accuracy averages, so those cover each batch once, as
+    # the single-process epoch does
+    out.ssip_padded = [b >= nb for b in range(blo, bhi)]
+    return out
 
 
 def gather_list(local: list) -> list:

@@ -187,13 +187,16 @@ def train_consistency(model, base, train_idx, pool, val_loader, criterion, devic
                                     even=True)
         lab_iter = iter(lab_loader)
         losses, yt, yp = [], [], []
-        for xu, _ in unl_loader:
+        padded = getattr(unl_loader, "ssip_padded", None)
+        for bi, (xu, _) in enumerate(unl_loader):
             try:
                 xl, yl = next(lab_iter)
             except StopIteration:
                 lab_iter = iter(lab_loader)
                 xl, yl = next(lab_iter)
             out = step(xl.to(device, non_blocking=True), yl.to(device), xu.to(device, non_blocking=True))
+            if padded is not None and padded[bi]:
+                continue  # a wrap-around repeat (shard_loader even=True): stepped, not averaged
             losses.append(out.loss[0:1].clone())
             yt.append(yl)
             yp.append(step.last["logits"][: yl.shape[0]].argmax(1).cpu())

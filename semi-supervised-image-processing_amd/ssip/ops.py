@@ -335,8 +335,13 @@ def conv_dgrad_bn(g: ConvGeom, dy: torch.Tensor, w_crsk: torch.Tensor, dx_add: O
     call(*args)
 
 
-def conv_wgrad_workspace_bytes(g: ConvGeom) -> int:
-    return int(_lib.lib().ssip_conv_wgrad_workspace_bytes(g.desc()))
+def conv_wgrad_workspace_bytes(g: ConvGeom, max_workgroups: int = 0) -> int:
+    """Workspace of conv_wgrad(g, ..., max_workgroups) (0: the full-chip grid)."""
+    key = ("ws", g, int(max_workgroups), _plan_env())
+    v = _plan_cache.get(key)
+    if v is None:
+        v = _plan_cache[key] = int(_lib.lib().ssip_conv_wgrad_workspace_bytes_budget(g.desc(), int(max_workgroups)))
+    return v
 
 
 def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, accumulate: bool,
@@ -359,10 +364,12 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
     call(*args)
 
 
-def conv_kernel_name(mode: str, g: ConvGeom, dtype: torch.dtype) -> str:
-    """The kernel ssip_conv_{fwd,dgrad,wgrad} selects for g (include/ssip.h)."""
+def conv_kernel_name(mode: str, g: ConvGeom, dtype: torch.dtype, max_workgroups: int = 0) -> str:
+    """The kernel ssip_conv_{fwd,dgrad,wgrad} selects for g (include/ssip.h);
+    max_workgroups: ssip_conv_wgrad_budget's choice under that budget."""
     buf = ctypes.create_string_buffer(160)
-    call("ssip_conv_kernel_name", {"fwd": 0, "dgrad": 1, "wgrad": 2}[mode], g.desc(), _DT[dtype], buf, 160)
+    call("ssip_conv_kernel_name_budget", {"fwd": 0, "dgrad": 1, "wgrad": 2}[mode], g.desc(), _DT[dtype],
+         int(max_workgroups), buf, 160)
     return buf.value.decode()
 
 

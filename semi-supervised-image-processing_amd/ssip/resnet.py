@@ -772,10 +772,11 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             break
 
     ws_bytes = 0
-    for recs, ds, _ in sv.blocks:
-        for r in recs + ([ds] if ds is not None else []):
-            ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(r.geom))
-    ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(sv.stem.geom))
+    budgeted = side is not None or WGRAD_BUDGET_SERIAL
+    for r in [r for recs, ds, _ in sv.blocks for r in recs + ([ds] if ds is not None else [])] + [sv.stem]:
+        ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(r.geom))
+        if budgeted:  # the side stream's grids may take more split slabs (ABI 12)
+            ws_bytes = max(ws_bytes, ops.conv_wgrad_workspace_bytes(r.geom, _side_wgrad_budget(r.geom, dt, dev)))
     workspace = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
     coef_buf = torch.empty(6 * 2048, device=dev, dtype=torch.float32)
 

@@ -146,6 +146,10 @@ def _pipeline_worker(rank, world, port, q):
             single_b = [list(range(b * bs, (b + 1) * bs)) for b in range(nb)]
             allb = [b for part in D.gather_list([got]) for b in part]
             ok &= allb == [single_b[i % nb] for i in range(len(allb))]
+            # the wrap-around repeats are flagged: the unflagged batches over all
+            # ranks are each single-process batch exactly once (epoch averages)
+            flags = [f for part in D.gather_list([even.ssip_padded]) for f in part]
+            ok &= len(flags) == len(allb) and sorted(b for b, f in zip(allb, flags) if not f) == single_b
         # rank 0's BN buffers on every rank, bitwise
         bn = torch.nn.Sequential(torch.nn.BatchNorm2d(5), torch.nn.BatchNorm2d(3))
         bn.train()

@@ -1,0 +1,54 @@
+"""Layer-1 halo conv lab (GPU box): the 3x3 / stride-1 / 64-channel forward and
+dgrad of ResNet-18 layer 1 (conv_halo_kernel) at batch 256 and 128, timed
+with HIP events, per SSIP_HALO_DIAG ablation (timing only, results wrong):
+0 full, 1 no output stores, 2 no MFMAs, 3 neither.  Speed of light per launch:
+max(FLOPs / 2.5 PF, (x + y bytes) / 8 TB/s).
+
+usage: python tools/halo_lab.py [--diags 0,1,2,3] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "semi-supervised-image-processing_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import torch  # noqa: E402
+from ssip import ops  # noqa: E402
+from tune_conv import time_fn  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--diags", default="0,1,2,3")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batches", default="256,128")
+    ap.add_argument("--tx", default="1,0", help="SSIP_HALO_TX values to compare")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    bf = torch.bfloat16
+    part = torch.empty(16 << 20, device=dev)
+    for n in [int(b) for b in a.batches.split(",")]:
+        g = ops.ConvGeom(n, 56, 56, 64, 64, 3, 3, 1, 1, 64, 3)
+        x = torch.randn(n, 56, 56, 64, device=dev).to(bf)
+        w = (torch.randn(64, 3, 3, 64, device=dev) * 0.05).to(bf)
+        wc = w.permute(3, 1, 2, 0).contiguous()
+        y = torch.empty(n, 56, 56, 64, device=dev, dtype=bf)
+        dx = torch.empty_like(x)
+        sol = max(g.flops() / 2.5e15, 2 * x.numel() * 2 / 8e12) * 1e6
+        print(f"batch {n}: {ops.conv_kernel_name('fwd', g, bf)} / {ops.conv_kernel_name('dgrad', g, bf)}; "
+              f"SoL {sol:.1f} us", flush=True)
+        for tx in a.tx.split(","):
+            os.environ["SSIP_HALO_TX"] = tx
+            for dg in a.diags.split(","):
+                os.environ["SSIP_HALO_DIAG"] = dg
+                tf = time_fn(lambda: ops.conv_fwd(g, x, w, y, part), a.iters)
+                td = time_fn(lambda: ops.conv_dgrad(g, y, wc, dx), a.iters)
+                print(f"  tx {tx} diag {dg}: fwd {tf:6.1f} us ({sol / tf:.2f} SoL, {g.flops() / tf / 1e6:4.0f} TF/s)"
+                      f"  dgrad {td:6.1f} us ({sol / td:.2f} SoL)", flush=True)
+        os.environ.pop("SSIP_HALO_DIAG", None)
+        os.environ.pop("SSIP_HALO_TX", None)
+
+
+if __name__ == "__main__":
+    main()

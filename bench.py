@@ -225,7 +225,7 @@ def extract_bench(args):
     print(json.dumps(out))
 
 
-def roofline_leg(step, x_l, y_l, x_u, kind, ops, resnet_mod, timer=True):
+def roofline_leg(step, x_l, y_l, x_u, kind, ops, resnet_mod, timer=True, lead=2):
     """One step with every launch on one stream and (timer) HIP events around
     every conv launch.  kind "full": the wgrads at their full-chip grids;
     "production": with the side stream's grid budgets.  Two unsynchronised
@@ -234,7 +234,7 @@ def roofline_leg(step, x_l, y_l, x_u, kind, ops, resnet_mod, timer=True):
     kernel's execution, not device idle time waiting for the host's next
     launch (the brackets agree with rocprofv3's kernel durations,
     profiles/r5_roofline_leg_*.txt)."""
-    for _ in range(2):
+    for _ in range(lead):
         step(x_l, y_l, x_u)
     t = ops.ConvTimer() if timer else None
     ops.set_conv_timer(t)
@@ -303,7 +303,9 @@ def main():
         step(x_l, y_l, x_u)
     if args.profile_leg:
         for _ in range(args.steps):
-            roofline_leg(step, x_l, y_l, x_u, args.profile_leg, ops, resnet_mod, timer=False)
+            # every step of the trace after the warm-up is a leg step (no lead-in
+            # replays): the profile tools take the last complete one
+            roofline_leg(step, x_l, y_l, x_u, args.profile_leg, ops, resnet_mod, timer=False, lead=0)
         print(f"profile-leg {args.profile_leg}: {args.steps} legs done", file=sys.stderr)
         return
     slots = step.input_slots()

@@ -1542,86 +1542,6 @@ struct WaveStats {
   }
 };
 
-// The same statistics for a transposed accumulator tile (conv_halo_kernel
-// TX): lane l holds, per row group i, CPL contiguous channels of ONE pixel
-// (pixel bit i of pmask), so a lane's count is its own valid pixels and the
-// 16 lanes of a channel group (equal l >> 4) merge in fixed order (Chan).
-template <int FM, int FN>
-struct LaneStatsT {
-  // running {n, mean, M2} per channel over the lane's valid pixels: each
-  // tile's (up to FM) pixels are reduced about their own mean, then merged
-  // (Chan) -- no shift registers (the kernel is at its VGPR limit)
-  static constexpr int CPL = 4 * FN;
-  float n, mean[CPL], m2[CPL];
-  __device__ __forceinline__ void reset() {
-    n = 0.f;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) mean[c] = m2[c] = 0.f;
-  }
-  __device__ __forceinline__ void tile(const f32x4 (&acc)[FM][FN], uint32_t pmask) {
-    const float nt = (float)__builtin_popcount(pmask);
-    if (nt == 0.f) return;
-    const float nn = n + nt, rt = 1.f / nt;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) s += ((pmask >> i) & 1u) ? acc[i][c >> 2][c & 3] : 0.f;
-      const float mt = s * rt;
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const float d = ((pmask >> i) & 1u) ? acc[i][c >> 2][c & 3] - mt : 0.f;
-        q = __builtin_fmaf(d, d, q);
-      }
-      const float d = mt - mean[c];
-      mean[c] = mean[c] + d * (nt / nn);
-      m2[c] = m2[c] + q + d * d * (n * nt / nn);
-    }
-    n = nn;
-  }
-  __device__ __forceinline__ void wave_merge(float& nw, float (&mo)[CPL], float (&qo)[CPL]) const {
-    nw = n;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      mo[c] = mean[c];
-      qo[c] = m2[c];
-    }
-#pragma unroll
-    for (int off = 1; off <= 8; off <<= 1) {
-      const float nb = __shfl_xor(nw, off, 64);
-      const float nn = nw + nb;
-      const bool lo = (threadIdx.x & off) == 0;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const float mb = __shfl_xor(mo[c], off, 64), qb = __shfl_xor(qo[c], off, 64);
-        const float na_ = lo ? nw : nb, ma = lo ? mo[c] : mb, qa = lo ? qo[c] : qb;
-        const float nb_ = lo ? nb : nw, mb_ = lo ? mb : mo[c], qb_ = lo ? qb : qo[c];
-        const float d = mb_ - ma;
-        mo[c] = nn > 0.f ? ma + d * (nb_ / nn) : 0.f;
-        qo[c] = nn > 0.f ? qa + qb_ + d * d * (na_ * nb_ / nn) : 0.f;
-      }
-      nw = nn;
-    }
-  }
-};
-
-// 8 fp32 -> 8 bf16 packed in 16 B (element c at bits 16 (c & 1) of dword c / 2)
-__device__ __forceinline__ i32x4 pack_bf16x8(const float (&v)[8]) {
-  i32x4 r;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t lo = __builtin_bit_cast(unsigned short, from_f32<__bf16>(v[2 * d]));
-    const uint32_t hi = __builtin_bit_cast(unsigned short, from_f32<__bf16>(v[2 * d + 1]));
-    r[d] = (int)(lo | (hi << 16));
-  }
-  return r;
-}
-__device__ __forceinline__ float bf16x8_get(const i32x4& r, int c) {
-  const uint32_t w = (uint32_t)r[c >> 1];
-  return to_f32(__builtin_bit_cast(__bf16, (unsigned short)((c & 1) ? (w >> 16) : (w & 0xFFFFu))));
-}
-
 struct HaloArgs {
   const __bf16* X;    // [N][H][W][64]   (FWD: x, DGRAD: dy)
   const __bf16* Wt;   // [Ncols][9][64]  (FWD: w_krsc, DGRAD: w_crsk)
@@ -1641,7 +1561,8 @@ struct HaloArgs {
   const uint8_t* pbits;
   const float *pmean, *pinvstd, *pmscale, *pmshift;
   uint32_t bits_bytes;
-  int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 1 no output stores, 2 no MFMAs
+  int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 1 no output stores, 2 no MFMAs,
+             // 4 no input-row DMA after the first tile, 8 no BN statistics
 };
 
 constexpr int HALO_XBUF = 44 * 1024;
@@ -1727,68 +1648,11 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
   }
 }
 
-// The BN-backward epilogue for the transposed tile (TX): lane l stores the 8
-// contiguous channels cb .. cb+7 of pixel (l & 15) of each row group as one
-// 16-B store; y / add are 16-B loads, the mask is the pixel's one mask byte
-// of those 8 channels (cb % 8 == 0).  Sums per channel in bsd / bsx.
-template <int FM, bool YONLY>
-__device__ __forceinline__ void halo_bnpost_epilogue_tx(const HaloArgs& a, const f32x4 (&acc)[FM][2],
-                                                        __amdgpu_buffer_rsrc_t rsO, __amdgpu_buffer_rsrc_t rsA,
-                                                        __amdgpu_buffer_rsrc_t rsY, __amdgpu_buffer_rsrc_t rsM,
-                                                        uint32_t obase, const uint32_t (&pxoff)[FM], uint32_t pmask,
-                                                        int c0, float (&bsd)[8], float (&bsx)[8]) {
-  const bool bits = !YONLY && a.pbits != nullptr;
-  const bool has_add = !YONLY && a.add != nullptr;
-  float mu[8], is[8], msc[8], msh[8];
-  load_f8(mu, a.pmean + c0);
-  load_f8(is, a.pinvstd + c0);
-  if (!bits) {
-    load_f8(msc, a.pmscale + c0);
-    load_f8(msh, a.pmshift + c0);
-  } else {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) msc[c] = msh[c] = 0.f;
-  }
-  i32x4 ry[FM], ra[FM];
-  uint32_t rm[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const uint32_t off = obase + pxoff[i];
-    const bool valid = (pmask >> i) & 1u;
-    ry[i] = __builtin_amdgcn_raw_buffer_load_b128(rsY, off, 0, 0);
-    ra[i] = has_add ? __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0) : (i32x4){0, 0, 0, 0};
-    rm[i] = bits ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsM, valid ? off >> 4 : SSIP_OOB, 0, 0) : 0u;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const bool valid = (pmask >> i) & 1u;
-    float o[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float yv = bf16x8_get(ry[i], c);
-      float t = to_f32(from_f32<__bf16>(acc[i][c >> 2][c & 3]));
-      if (has_add) t += bf16x8_get(ra[i], c);
-      const bool keep = bits ? ((rm[i] >> c) & 1u) != 0u : __builtin_fmaf(yv, msc[c], msh[c]) > 0.f;
-      o[c] = to_f32(from_f32<__bf16>(keep ? t : 0.f));
-      const float dq = valid ? o[c] : 0.f;
-      bsd[c] += dq;
-      bsx[c] += dq * ((yv - mu[c]) * is[c]);
-    }
-    __builtin_amdgcn_raw_buffer_store_b128(pack_bf16x8(o), rsO, obase + pxoff[i], 0, 0);
-  }
-}
-
 // BNPOST: 0 = none; 1 = the BN-backward post-op with no residual add and the
 // mask from the BN affine (y is the only extra operand: one load batch per
 // tile); 2 = any other post-op operand set (one load batch per row group:
 // the registers hold no more without spilling)
-// TX: the transposed MFMA (D[channel][pixel] = W * X^T), with the weight
-// panel's rows permuted so lane l's accumulators are CPL = 8 contiguous
-// channels of one pixel: every output row piece is stored as one 16-B lane
-// store, 64 contiguous bytes per pixel and instruction (the untransposed form
-// stores 2 B per lane, 32-B row pieces: VERDICT r4 item 5's write-request
-// audit).  Same products in the same order: the same bits.
-template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool TX = false>
+template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, NT = 64 * NW;
@@ -1797,7 +1661,6 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   constexpr int B_BYTES = 9 * BN * 128;
   static_assert(FM >= 1 && FN >= 1 && (NW == 4 || NW == 8 || NW == 16) && WMW <= HALO_WMW, "bad halo wave tile");
   static_assert(B_BYTES + 2 * HALO_XBUF <= 160 * 1024, "LDS");
-  static_assert(!TX || FN == 2, "TX: 8 channels per lane");
   __shared__ __attribute__((aligned(16))) char smem[B_BYTES + 2 * HALO_XBUF];
   char* const Bs = smem;
 
@@ -1831,11 +1694,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     for (int i = wave; i < 72; i += NW) {
       const int tw = i >> 3, col = ((i & 7) << 3) + (lane >> 3);
       const int ch = (lane & 7) ^ ((col >> 1) & 7);
-      // TX: LDS row col = 16 jj + 4 kq + e of wave column wn holds channel
-      // wn WTN + 8 kq + 4 jj + e (the lane's 8 contiguous channels)
-      const int rl = col % WTN;
-      const int src = TX ? (col - rl) + 8 * ((rl >> 2) & 3) + 4 * (rl >> 4) + (rl & 3) : col;
-      const uint32_t off = (uint32_t)(((((long)jn * 64 + src) * 9 + tw) * 64 + ch * 8) * 2);
+      const uint32_t off = (uint32_t)(((((long)jn * 64 + col) * 9 + tw) * 64 + ch * 8) * 2);
       blds16(rsW, off, Bs + i * 1024);
     }
   };
@@ -1869,31 +1728,10 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   float bsd[FN], bsx[FN];
 #pragma unroll
   for (int jj = 0; jj < FN; ++jj) bsd[jj] = bsx[jj] = 0.f;
-  float tbsd[8], tbsx[8];  // TX: the lane's 8 channels
-#pragma unroll
-  for (int c = 0; c < 8; ++c) tbsd[c] = tbsx[c] = 0.f;
   const __amdgpu_buffer_rsrc_t rsY = make_rsrc(a.py, BNPOST ? a.o_bytes : 0);
   const __amdgpu_buffer_rsrc_t rsM = make_rsrc(a.pbits, BNPOST ? a.bits_bytes : 0);
   WaveStats<FM, FN> ws;
   ws.reset();
-  LaneStatsT<FM, FN> wst;
-  wst.reset();
-  // TX: this lane's pixel per row group (wm WTM + 16 i + (l & 15)) and its
-  // first channel (wn WTN + 8 kq)
-  const int c8 = wn * WTN + 8 * kq;
-  // (recomputed per tile in the epilogue: kept across the k-loop they cost
-  // the registers that made the forward spill)
-  auto tx_pixels = [&](uint32_t (&pxoff)[FM], uint32_t& pmask) {
-    pmask = 0;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = wm * WTM + i * 16 + (lane & 15);
-      const int j = m / Wp, q = m - j * Wp;
-      const bool v = m < mrows && q < a.W;
-      pxoff[i] = v ? (uint32_t)(((j * a.W + q) * a.Ncols + c8) * 2) : 0x80000000u;
-      pmask |= (v ? 1u : 0u) << i;
-    }
-  };
   // this lane's output rows (rbase + 16 i + e): byte offset within a tile's
   // output block and validity (q < W of the padded grid), fixed for all tiles
   const int rbase = wm * WTM + kq * 4, cbase = wn * WTN + (lane & 15);
@@ -1937,7 +1775,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     const bool more = un < u1;
     const int jn_next = more ? un / a.tiles : jn;
     const bool prefetch = more && jn_next == jn;
-    if (prefetch) issue_x(un - jn * a.tiles, Xn);  // tile u-1's buffer: every wave is past its reads
+    if (prefetch && !(a.diag & 4)) issue_x(un - jn * a.tiles, Xn);  // tile u-1's buffer: every wave is past its reads
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -1968,10 +1806,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int jj = 0; jj < FN; ++jj) {
-          if constexpr (TX) mma(acc[i][jj], fb[st & 1][jj], fa[st & 1][i]);
-          else mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
-        }
+        for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
     }
     if (a.diag & 2) {  // keep the fragment reads alive
 #pragma unroll
@@ -1982,41 +1817,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---- epilogue
-    uint32_t pxoff[FM], pmask = 0;
-    if constexpr (TX) tx_pixels(pxoff, pmask);
-    if constexpr (BNPOST && TX) {
-      if (!(a.diag & 1))
-        halo_bnpost_epilogue_tx<FM, BNPOST == 1>(a, acc, rsO, rsA, rsY, rsM,
-                                                 (uint32_t)(((long)tile * rows * a.Ncols + jn * BN) * 2), pxoff, pmask,
-                                                 jn * BN + c8, tbsd, tbsx);
-      if (!prefetch) {
-        // panel / range end: the 16 lanes of each channel group -> records [c][g][wm]
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-#pragma unroll
-          for (int off = 1; off <= 8; off <<= 1) {
-            tbsd[c] += __shfl_xor(tbsd[c], off, 64);
-            tbsx[c] += __shfl_xor(tbsx[c], off, 64);
-          }
-        if ((lane & 15) == 0) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            float* rec = a.partial + ((long)(jn * BN + c8 + c) * G * HALO_WMW + (long)g * HALO_WMW + wm) * 2;
-            rec[0] = tbsd[c];
-            rec[1] = tbsx[c];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 8; ++c) tbsd[c] = tbsx[c] = 0.f;
-      }
-      if (more && !prefetch) {
-        halo_lds_barrier();
-        issue_w(jn_next);
-        issue_x(un - jn_next * a.tiles, Xn);
-        first = true;
-      }
-      continue;
-    } else if constexpr (BNPOST) {
+    if constexpr (BNPOST) {
       halo_bnpost_epilogue<FM, FN, BNPOST == 1 ? FM : 1, BNPOST == 1>(a, acc, rsO, rsA, rsY, rsM, tile, rows,
                                                                           jn * BN, rowoff, vmask, cbase, bsd, bsx);
       if (!prefetch) {
@@ -2048,25 +1849,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
       }
       continue;
     }
-    if constexpr (TX) {
-     if (a.partial && wrows > 0) {
-      wst.tile(acc, pmask);
-      if (!prefetch) {
-        float n, mean[8], m2[8];
-        wst.wave_merge(n, mean, m2);
-        if ((lane & 15) == 0) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            float* rec = a.partial + ((long)(jn * BN + c8 + c) * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
-            rec[0] = n;
-            rec[1] = mean[c] * n;
-            rec[2] = m2[c];
-          }
-        }
-        wst.reset();
-      }
-     }
-    } else if (a.partial && wrows > 0) {
+    if (a.partial && wrows > 0 && !(a.diag & 8)) {
       // per-lane shifted sums over the fp32 accumulators of the valid rows;
       // merged across the wave (and written) when the panel or range ends
       ws.tile(acc, vmask);
@@ -2086,38 +1869,12 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
         ws.reset();
       }
     }
-    if constexpr (TX) {
-     if (!(a.diag & 1)) {
-      // one 16-B store per lane and row group: 8 contiguous channels of its
-      // pixel (padded-grid pixels go to an out-of-range offset)
-      const uint32_t obase = (uint32_t)(((long)tile * rows * a.Ncols + jn * BN) * 2);
-      float bcol[8];
-      if constexpr (FOLD) load_f8(bcol, a.bias + jn * BN + c8);
-      const float lo = (FOLD && a.relu) ? 0.f : -__builtin_huge_valf();
-      i32x4 r[FM];
-      if (a.add) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) r[i] = __builtin_amdgcn_raw_buffer_load_b128(rsA, obase + pxoff[i], 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        float o[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const float v = acc[i][c >> 2][c & 3];
-          if (a.add) {
-            const float t = to_f32(from_f32<T>(FOLD ? v + bcol[c] : v)) + bf16x8_get(r[i], c);
-            o[c] = FOLD ? fmaxf(t, lo) : t;
-          } else {
-            o[c] = FOLD ? fmaxf(v + bcol[c], lo) : v;
-          }
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(pack_bf16x8(o), rsO, obase + pxoff[i], 0, 0);
-      }
-     }
-    } else if (!(a.diag & 1)) {
+    if (!(a.diag & 1)) {
       // 16-bit stores straight from the accumulators (lane: 4 rows x 1 column
-      // per fragment; padded-grid rows go to an out-of-range offset)
+      // per fragment; padded-grid rows go to an out-of-range offset).  Round 5
+      // measured them at 3 us of a 78 us layer-1 forward (SSIP_HALO_DIAG=1,
+      // profiles/r5_halo_lab.txt), and a transposed tile with 16-B row stores
+      // at 93 us: the 32-B pieces are not what bounds this kernel.
       const uint32_t obase = (uint32_t)(((long)tile * rows * a.Ncols + jn * BN) * 2);
       uint32_t off[FM][4];
 #pragma unroll
@@ -2962,9 +2719,14 @@ static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st);
 static int device_cus();
-static bool wgrad_big_enabled() {
+// SSIP_WGRAD_BIG: 1 = the budget's 16-wave 256-column tiles for every 3x3
+// wgrad, 2 = only the 256x256 ones (K % 256 == 0); unset / 0 = the full-grid
+// tiles (default: faster alone, but the step measured 6.34 vs 6.19 ms with
+// them -- a 16-wave workgroup holding every register of its CU keeps the main
+// stream's dgrad / BN chain off it; profiles/r5_wgrad_lab.txt, r5_ab.txt)
+static int wgrad_big_mode() {
   const char* e = getenv("SSIP_WGRAD_BIG");
-  return !(e && e[0] == '0');
+  return e ? atoi(e) : 0;
 }
 
 // Default LDS-DMA configuration for a bf16 GEMM view (M x Ng, reduction Kg).
@@ -3067,12 +2829,13 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   // workgroups of 256 columns hide that and halve the DMA bytes per FLOP
   // (tools/wgrad_lab.py at the 256-workgroup budget, profiles/r5_wgrad_lab.txt:
   // l2.3x3 110.9 -> 89.1 us with 128x256, l3.3x3 109.9 -> 73.9 and l4.3x3
-  // 101.4 -> 75.4 with 256x256; SSIP_WGRAD_BIG=0 keeps the 128x128 tiles)
-  if (mode == MODE_WGRAD && wg_budget > 0 && pl.stages > 0 && !pl.conv1 && wgrad_big_enabled()) {
+  // 101.4 -> 75.4 with 256x256) -- but not in the step (wgrad_big_mode)
+  const int bigm = mode == MODE_WGRAD ? wgrad_big_mode() : 0;
+  if (mode == MODE_WGRAD && wg_budget > 0 && pl.stages > 0 && !pl.conv1 && bigm > 0) {
     // (the 1x1 downsample wgrads, Ng <= 256, keep their many-tile grids)
     if (a.M % 256 == 0 && a.Ng % 256 == 0 && a.Ng >= 512) {
       pl.bm = 256; pl.bn = 256; pl.wmw = 4; pl.wnw = 4;
-    } else if (a.M % 128 == 0 && a.Ng >= 512) {
+    } else if (bigm == 1 && a.M % 128 == 0 && a.Ng >= 512) {
       pl.bm = 128; pl.bn = 256; pl.wmw = 4; pl.wnw = 4;  // a partial last tile where Ng % 256 != 0
     }
   }
@@ -3476,18 +3239,7 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   // 8 waves of 64x32 (16 waves of 32x32 were ~10 % faster in isolation but 3 %
   // slower in the step, where the side streams' kernels run beside them; 4
   // waves of 64x64 slower still: r3-variants branch)
-  // TX (default; SSIP_HALO_TX=0: the untransposed epilogue) -- conv_halo_kernel
-  const char* tx = getenv("SSIP_HALO_TX");
-  if (!(tx && tx[0] == '0')) {
-    if (bp != nullptr && add == nullptr && bp->bits == nullptr)
-      hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 1, true>), dim3(hp.G), dim3(512), 0, st, h);
-    else if (bp != nullptr)
-      hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
-    else if (bias != nullptr)
-      hipLaunchKernelGGL((conv_halo_kernel<4, 2, true, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
-    else
-      hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
-  } else if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
+  if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bp != nullptr)
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);

@@ -185,7 +185,7 @@ _plan_cache = {}
 
 
 def _plan_env():
-    return (os.environ.get("SSIP_HALO"), os.environ.get("SSIP_CONV_FORCE"))
+    return tuple(os.environ.get(k) for k in ("SSIP_HALO", "SSIP_CONV_FORCE", "SSIP_WGRAD_BIG"))
 
 
 def conv_fwd_partial_floats(g: ConvGeom) -> int:

@@ -484,7 +484,12 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
     Wp = (g.Q + 2 * pd - k) // s + 1
     pool = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt)
     idx = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=torch.uint8)
-    # BN -> ReLU -> max-pool in one pass over y (the full-resolution z is never stored)
+    # BN -> ReLU -> max-pool in one pass over y (the full-resolution z is never
+    # stored).  (Round 5 measured the window selection inside the stem conv --
+    # conv rows 2p-1..2p+1 per pooled row, BN + ReLU after on the pooled grid,
+    # no y read -- at 429 us vs 164 + 180 for the two kernels: the per-element
+    # selection and statistics VALU work inside the conv costs more than the
+    # y read it saves; profiles/r5_stem_pool_lab.txt)
     ymax = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt) if save else None
     ops.stem_bn_pool_fwd(N, g.P, g.Q, g.K, k, s, pd, rec.y, rec.stats[2], rec.stats[3], pool, idx, ymax)
     if save:

@@ -20,10 +20,10 @@ from tune_conv import time_fn  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--diags", default="0,1,2,3")
+    ap.add_argument("--diags", default="0,1,2,3,4,8,12")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batches", default="256,128")
-    ap.add_argument("--tx", default="1,0", help="SSIP_HALO_TX values to compare")
+    ap.add_argument("--tx", default="0", help="(round 5 TX variant: removed; kept for the command line)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
@@ -47,7 +47,31 @@ def main():
                 print(f"  tx {tx} diag {dg}: fwd {tf:6.1f} us ({sol / tf:.2f} SoL, {g.flops() / tf / 1e6:4.0f} TF/s)"
                       f"  dgrad {td:6.1f} us ({sol / td:.2f} SoL)", flush=True)
         os.environ.pop("SSIP_HALO_DIAG", None)
-        os.environ.pop("SSIP_HALO_TX", None)
+        # the stem conv (conv_stem_halo_kernel): pre-padded 230x230x4 image, 7x7/2 -> 112x112x64
+        gs = ops.ConvGeom(n, 230, 230, 4, 64, 7, 8, 2, 0, 3, 7)
+        xs = torch.randn(n, 230, 230, 4, device=dev).to(bf)
+        ws_ = (torch.randn(64, 7, 8, 4, device=dev) * 0.05).to(bf)
+        ys = torch.empty(n, 112, 112, 64, device=dev, dtype=bf)
+        ssol = max(gs.flops() / 2.5e15, (xs.numel() + ys.numel()) * 2 / 8e12) * 1e6
+        t = time_fn(lambda: ops.conv_fwd(gs, xs, ws_, ys, part), a.iters)
+        print(f"  stem {ops.conv_kernel_name('fwd', gs, bf)}: {t:6.1f} us ({ssol / t:.2f} of SoL "
+              f"{ssol:.1f} us)", flush=True)
+        sc = torch.rand(64, device=dev) + 0.5
+        sh = torch.randn(64, device=dev) * 0.1
+        pool = torch.empty(n, 56, 56, 64, device=dev, dtype=bf)
+        pidx = torch.empty(n, 56, 56, 64, device=dev, dtype=torch.uint8)
+        ymx = torch.empty_like(pool)
+        tp = time_fn(lambda: ops.stem_bn_pool_fwd(n, 112, 112, 64, 3, 2, 1, ys, sc, sh, pool, pidx, ymx), a.iters)
+        print(f"  stem_bn_pool_fwd (unfused pool pass): {tp:6.1f} us", flush=True)
+        gam = torch.randn(64, device=dev)
+        for label, yy, pp in (("y+stats", ys, part), ("stats", None, part), ("y", ys, None), ("none", None, None)):
+            for dg in ("0", "1", "2", "4", "7"):
+                os.environ["SSIP_STEM_POOL_DIAG"] = dg
+                t2 = time_fn(lambda: ops.stem_conv_pool(gs, xs, ws_, gam, yy, ymx, pidx, pp), a.iters)
+                print(f"  stem_conv_pool [{label}] diag {dg}: {t2:6.1f} us", flush=True)
+        os.environ.pop("SSIP_STEM_POOL_DIAG", None)
+        ta = time_fn(lambda: ops.bn_apply(n * 56 * 56, 64, ymx, sc, sh, None, True, pool), a.iters)
+        print(f"  pooled bn_apply: {ta:6.1f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -14,10 +14,11 @@ import collections, csv, json, sys
 
 
 def family(n):
-    for k in ("conv_gemm_kernel", "conv_glds_kernel", "conv_halo_kernel", "conv_stem_halo_kernel",
-              "conv_halo_wgrad_kernel", "conv_stem_wgrad_kernel", "conv_stem_bwd_wgrad_kernel"):
-        if k in n:
-            return "conv"
+    # every conv kernel (conv_glds / conv_gemm / conv_halo / conv_stem_halo /
+    # conv_halo_wgrad / conv_stem_wgrad / conv_stem_bwd_wgrad2 -- round 4's list
+    # missed the last one's "2" and counted it under "stem")
+    if "conv_" in n and "_kernel" in n:
+        return "conv"
     if "wgrad_reduce" in n:
         return "conv"  # the wgrad split-K reduce belongs to the conv family (as in bench.py's roofline)
     for k in ("stem_", "bn_", "maxpool", "augment", "adamw", "avgpool", "weight_prep", "semi_loss"):

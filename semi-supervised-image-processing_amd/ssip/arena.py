@@ -23,8 +23,11 @@ class ParamArena:
                 raise TypeError("ParamArena: all parameters must be fp32 on one device")
         self.params = list(params)
         total = sum(p.numel() for p in params)
-        self.flat = torch.empty(total, device=dev, dtype=torch.float32)
-        self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
+        # padded to 64 floats: gradient buckets end on a 16-B multiple (RCCL
+        # 2.26's ncclPreMulSum leaves a count % 4 tail unscaled, ssip/dist.py)
+        self.padded = -(-total // 64) * 64
+        self.flat = torch.zeros(self.padded, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(self.padded, device=dev, dtype=torch.float32)
         self.offsets: Dict[int, Tuple[int, int]] = {}
         off = 0
         with torch.no_grad():

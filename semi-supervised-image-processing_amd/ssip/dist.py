@@ -83,6 +83,20 @@ class GradBucketer:
             lo = min(spans[i][0] for i in idxs)
             hi = max(spans[i][0] + spans[i][1] for i in idxs)
             self.ranges.append((lo, hi))
+        # Every bucket a multiple of 4 floats: RCCL 2.26.6's ncclPreMulSum
+        # (premul != 1) leaves the last count % 4 elements of a call unscaled
+        # (tools/rccl_premul_probe.py: the 2-float fc bias at the end of a
+        # 2,361,346-float bucket).  A boundary moves UP to a multiple of 4, so
+        # the up-to-3 boundary floats (the lowest parameter of the bucket
+        # above, produced earlier in the backward) join the bucket below,
+        # which launches later: still reduced once, after they are complete.
+        # The first bucket ends at the arena's padded end (zeros).
+        end = getattr(arena, "padded", arena.numel)
+        for b in range(len(self.ranges)):
+            lo, hi = self.ranges[b]
+            hi = end if b == 0 else self.ranges[b - 1][0]
+            lo = lo if lo == 0 else -(-lo // 4) * 4
+            self.ranges[b] = (lo, hi)
         # hipGraph mode (SemiStep(graph=True)): the backward is captured
         # without collectives (ROCm allows no external event nodes in a graph,
         # so a bucket cannot signal mid-replay); after each replay

@@ -182,3 +182,30 @@ def test_pipeline_sharding_world2():
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: True, 1: True}
     assert all(p.exitcode == 0 for p in procs)
+
+
+def test_bucket_ranges_cover_arena_in_multiples_of_four():
+    """GradBucketer's ranges: the padded arena exactly once, every bucket a
+    multiple of 4 floats (RCCL's PreMulSum tail), and every parameter element
+    in a bucket that launches no earlier than the parameter's own (a boundary
+    float may only move to a LATER bucket: lower addresses, reduced after the
+    bucket it came from, when it is already complete)."""
+    import torch
+
+    from ssip import SSIPResNet, replace_fc
+    from ssip.dist import GradBucketer
+
+    m = replace_fc(SSIPResNet("resnet18", 1000), 2)
+    ar = m.flatten_parameters()
+    for bb in (8 << 20, 16 << 20, 3 << 20):
+        bk = GradBucketer(ar, bucket_bytes=bb)
+        cover = torch.zeros(ar.padded, dtype=torch.int32)
+        owner = torch.full((ar.padded,), -1, dtype=torch.int64)
+        for b, (lo, hi) in enumerate(bk.ranges):
+            assert (hi - lo) % 4 == 0 and lo < hi
+            cover[lo:hi] += 1
+            owner[lo:hi] = b
+        assert int(cover.min()) == 1 and int(cover.max()) == 1
+        for p in ar.params:
+            off, n = ar.span(p)
+            assert int(owner[off:off + n].min()) >= bk.bucket_of[id(p)]

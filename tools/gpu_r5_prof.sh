@@ -26,4 +26,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $out/$c -o run -- \
     python bench.py --steps 3 --warmup 3 --no-cpu-baseline --exec eager "${extra[@]}" > $out/$c.log 2>&1 || { tail -20 $out/$c.log; exit 1; }
 done
+timeout -k 10 300 python bench.py --dtype fp32 --steps 5 --warmup 2 --no-cpu-baseline > $out/bench_fp32.log 2>&1 || { tail -20 $out/bench_fp32.log; exit 1; }
+tail -1 $out/bench_fp32.log | cut -c1-400
 echo "prof $tag done"

@@ -1,10 +1,11 @@
 """Layer-1 halo conv lab (GPU box): the 3x3 / stride-1 / 64-channel forward and
 dgrad of ResNet-18 layer 1 (conv_halo_kernel) at batch 256 and 128, timed
 with HIP events, per SSIP_HALO_DIAG ablation (timing only, results wrong):
-0 full, 1 no output stores, 2 no MFMAs, 3 neither.  Speed of light per launch:
+0 full, 1 no output stores, 2 no MFMAs, 4 no input-row DMA after the first
+tile, 8 no BN statistics (bits combine).  Speed of light per launch:
 max(FLOPs / 2.5 PF, (x + y bytes) / 8 TB/s).
 
-usage: python tools/halo_lab.py [--diags 0,1,2,3] [--iters 20]
+usage: python tools/halo_lab.py [--diags 0,1,2,3,4,8,12] [--iters 20]
 """
 import argparse
 import os
@@ -23,7 +24,6 @@ def main():
     ap.add_argument("--diags", default="0,1,2,3,4,8,12")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batches", default="256,128")
-    ap.add_argument("--tx", default="0", help="(round 5 TX variant: removed; kept for the command line)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
@@ -38,14 +38,12 @@ def main():
         sol = max(g.flops() / 2.5e15, 2 * x.numel() * 2 / 8e12) * 1e6
         print(f"batch {n}: {ops.conv_kernel_name('fwd', g, bf)} / {ops.conv_kernel_name('dgrad', g, bf)}; "
               f"SoL {sol:.1f} us", flush=True)
-        for tx in a.tx.split(","):
-            os.environ["SSIP_HALO_TX"] = tx
-            for dg in a.diags.split(","):
-                os.environ["SSIP_HALO_DIAG"] = dg
-                tf = time_fn(lambda: ops.conv_fwd(g, x, w, y, part), a.iters)
-                td = time_fn(lambda: ops.conv_dgrad(g, y, wc, dx), a.iters)
-                print(f"  tx {tx} diag {dg}: fwd {tf:6.1f} us ({sol / tf:.2f} SoL, {g.flops() / tf / 1e6:4.0f} TF/s)"
-                      f"  dgrad {td:6.1f} us ({sol / td:.2f} SoL)", flush=True)
+        for dg in a.diags.split(","):
+            os.environ["SSIP_HALO_DIAG"] = dg
+            tf = time_fn(lambda: ops.conv_fwd(g, x, w, y, part), a.iters)
+            td = time_fn(lambda: ops.conv_dgrad(g, y, wc, dx), a.iters)
+            print(f"  diag {dg}: fwd {tf:6.1f} us ({sol / tf:.2f} SoL, {g.flops() / tf / 1e6:4.0f} TF/s)"
+                  f"  dgrad {td:6.1f} us ({sol / td:.2f} SoL)", flush=True)
         os.environ.pop("SSIP_HALO_DIAG", None)
         # the stem conv (conv_stem_halo_kernel): pre-padded 230x230x4 image, 7x7/2 -> 112x112x64
         gs = ops.ConvGeom(n, 230, 230, 4, 64, 7, 8, 2, 0, 3, 7)
@@ -63,13 +61,6 @@ def main():
         ymx = torch.empty_like(pool)
         tp = time_fn(lambda: ops.stem_bn_pool_fwd(n, 112, 112, 64, 3, 2, 1, ys, sc, sh, pool, pidx, ymx), a.iters)
         print(f"  stem_bn_pool_fwd (unfused pool pass): {tp:6.1f} us", flush=True)
-        gam = torch.randn(64, device=dev)
-        for label, yy, pp in (("y+stats", ys, part), ("stats", None, part), ("y", ys, None), ("none", None, None)):
-            for dg in ("0", "1", "2", "4", "7"):
-                os.environ["SSIP_STEM_POOL_DIAG"] = dg
-                t2 = time_fn(lambda: ops.stem_conv_pool(gs, xs, ws_, gam, yy, ymx, pidx, pp), a.iters)
-                print(f"  stem_conv_pool [{label}] diag {dg}: {t2:6.1f} us", flush=True)
-        os.environ.pop("SSIP_STEM_POOL_DIAG", None)
         ta = time_fn(lambda: ops.bn_apply(n * 56 * 56, 64, ymx, sc, sh, None, True, pool), a.iters)
         print(f"  pooled bn_apply: {ta:6.1f} us", flush=True)
 

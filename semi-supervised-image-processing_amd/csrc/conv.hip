@@ -1515,6 +1515,23 @@ struct WaveStats {
         }
     n += (float)__builtin_popcount(vmask);
   }
+  // tile() one row group at a time (i = 0 first): the same sums in the same order
+  __device__ __forceinline__ void rows(const f32x4 (&acc)[FM][FN], uint32_t vmask, int i) {
+    if (i == 0) {
+      if (n == 0.f)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj) k[jj] = acc[0][jj][0];
+      n += (float)__builtin_popcount(vmask);
+    }
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = ((vmask >> (i * 4 + e)) & 1) ? acc[i][jj][e] - k[jj] : 0.f;
+        s1[jj] += d;
+        s2[jj] = __builtin_fmaf(d, d, s2[jj]);
+      }
+  }
   __device__ __forceinline__ void wave_merge(float& nw, float (&mean)[FN], float (&m2)[FN]) const {
     nw = n;
 #pragma unroll
@@ -1561,8 +1578,8 @@ struct HaloArgs {
   const uint8_t* pbits;
   const float *pmean, *pinvstd, *pmscale, *pmshift;
   uint32_t bits_bytes;
-  int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 1 no output stores, 2 no MFMAs,
-             // 4 no input-row DMA after the first tile, 8 no BN statistics
+  int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 4 no input-row DMA after the
+             // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt)
 };
 
 constexpr int HALO_XBUF = 44 * 1024;
@@ -1652,7 +1669,7 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
 // mask from the BN affine (y is the only extra operand: one load batch per
 // tile); 2 = any other post-op operand set (one load batch per row group:
 // the registers hold no more without spilling)
-template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0>
+template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool ADD = false>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, NT = 64 * NW;
@@ -1707,6 +1724,19 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     pxb[i] = m < mrows ? m : 0;  // row m of the padded grid reads LDS pixel m + tap offset
   }
   const int kq = lane >> 4;
+  // A-fragment LDS offsets of the first 32-channel half, per row group and
+  // k-step tap (DGRAD: flipped), fixed for all tiles: 9 FM registers.  The
+  // second half is the same pixel at slot ^ 4, i.e. offset ^ 64 (xtile_off's
+  // swizzle only XORs the slot, and the buffer bases are multiples of 128):
+  // one v_xor per read instead of 9 FM more hoisted offsets.
+  uint32_t offA[FM][9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int tt = a.flip ? 8 - t : t;
+    const int toff = (tt / 3) * Wp + (tt % 3);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) offA[i][t] = (uint32_t)xtile_off(pxb[i] + toff, kq);
+  }
   int boff[FN][2];
 #pragma unroll
   for (int jj = 0; jj < FN; ++jj)
@@ -1755,6 +1785,59 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     issue_w(jn);
     issue_x(u0 - jn * a.tiles, smem + B_BYTES);
   }
+  const bool stats = a.partial && wrows > 0 && !(a.diag & 8);
+  constexpr bool has_add = ADD;  // BNPOST == 0: out += add (BNPOST reads a.add itself)
+  // The epilogue of one row group i of a finished tile: BN statistics over the
+  // fp32 accumulators of its valid rows, then 16-bit stores straight from the
+  // accumulators (lane: 4 rows x 1 column per fragment; padded-grid rows go to
+  // an out-of-range offset), with the residual (ra, loaded beforehand) and the
+  // folded eval BN bias / ReLU applied.  Round 5 measured the stores at 3 us
+  // of a 78 us layer-1 forward and a transposed tile with 16-B row stores at
+  // 93 us (profiles/r5_halo_lab.txt): the 32-B pieces do not bound the kernel.
+  auto epi_rows = [&](const f32x4 (&ac)[FM][FN], int i, int etile, int ejn, const short (&ra)[FM][FN][4]) {
+    if (stats) ws.rows(ac, vmask, i);
+    const uint32_t obase = (uint32_t)(((long)etile * rows * a.Ncols + ejn * BN) * 2);
+    const float lo = (FOLD && a.relu) ? 0.f : -__builtin_huge_valf();
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) {
+      const float bcol = FOLD ? a.bias[ejn * BN + cbase + jj * 16] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t off = obase + rowoff[i][e] + jj * 32;
+        float t = FOLD ? ac[i][jj][e] + bcol : ac[i][jj][e];
+        if (has_add) t = to_f32(from_f32<T>(t)) + to_f32(__builtin_bit_cast(T, ra[i][jj][e]));
+        const T o = from_f32<T>(FOLD ? fmaxf(t, lo) : t);
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off, 0, 0);
+      }
+    }
+  };
+  auto epi_load = [&](int etile, int ejn, short (&ra)[FM][FN][4]) {
+    const uint32_t obase = (uint32_t)(((long)etile * rows * a.Ncols + ejn * BN) * 2);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          ra[i][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsA, obase + rowoff[i][e] + jj * 32, 0, 0);
+  };
+  // panel / range end: the wave's BN sums -> records [c][g][wm]
+  auto stats_flush = [&](int ejn) {
+    float n, mean[FN], m2[FN];
+    ws.wave_merge(n, mean, m2);
+    if (lane < 16) {
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) {
+        const int c = ejn * BN + cbase + jj * 16;
+        float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
+        rec[0] = n;
+        rec[1] = mean[jj] * n;
+        rec[2] = m2[jj];
+      }
+    }
+    ws.reset();
+  };
+
   // One barrier per tile: after it every wave has finished the previous
   // tile's fragment reads (so that buffer may take the next rows) and has
   // seen its own share of this tile's rows land (the vmcnt(0) each wave
@@ -1762,7 +1845,11 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   // MFMA phase).  The epilogue writes straight from the accumulators with
   // 16-bit buffer stores and needs no LDS, so a wave that finishes its MFMAs
   // early runs its epilogue while the other waves still compute, and its
-  // stores stay in flight into the next tile.
+  // stores stay in flight into the next tile.  (Round 5 deferred each tile's
+  // epilogue into the next tile's MFMAs, one row group per 4 k-steps: the 32
+  // accumulators it keeps push the kernel past 256 VGPRs into spills, 132 vs
+  // 82 us; profiles/r5_halo_lab.txt.)
+  short rap[FM][FN][4];
   bool first = true;
   for (int u = u0; u < u1; ++u) {
     const int jn = u / a.tiles, tile = u - jn * a.tiles;
@@ -1787,14 +1874,18 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     // Fragments are read one k-step ahead (register double buffer) so the
     // LDS latency hides behind the previous step's MFMAs.
     Frag<T> fa[2][FM], fb[2][FN];
+    const uint32_t xbase = (uint32_t)(Xs - smem);
+    uint32_t m64 = 64;  // opaque per tile: keeps offA ^ 64 from being hoisted into 9 FM more registers
+    asm volatile("" : "+s"(m64));
+    uint32_t xa[FM];
     auto load_step = [&](int st, Frag<T>(&ra)[FM], Frag<T>(&rb)[FN]) {
       const int t = st >> 1, kh = st & 1;
-      const int tt = a.flip ? 8 - t : t;
-      const int toff = (tt / 3) * Wp + (tt % 3);
       const char* bt = Bs + t * (BN * 128);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        ra[i].v = *reinterpret_cast<const bf16x8*>(Xs + xtile_off(pxb[i] + toff, 4 * kh + kq));
+      for (int i = 0; i < FM; ++i) {
+        xa[i] = kh ? xa[i] ^ m64 : xbase + offA[i][t];
+        ra[i].v = *reinterpret_cast<const bf16x8*>(smem + xa[i]);
+      }
 #pragma unroll
       for (int jj = 0; jj < FN; ++jj) rb[jj].v = *reinterpret_cast<const bf16x8*>(bt + boff[jj][kh]);
     };
@@ -1802,15 +1893,15 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
     for (int st = 0; st < 18; ++st) {
       if (st + 1 < 18) load_step(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
-      if (a.diag & 2) continue;
+      // step st + 1's fragment reads go out before step st's MFMAs: with the
+      // k-loop one basic block the scheduler otherwise sinks each read to just
+      // before its first use (lgkmcnt(0) ahead of most MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
-    }
-    if (a.diag & 2) {  // keep the fragment reads alive
-#pragma unroll
-      for (int i = 0; i < FM; ++i) acc[i][0][0] += (float)fa[1][i].v[0] + (float)fb[1][0].v[0];
+      __builtin_amdgcn_sched_barrier(0);
     }
     // the next tile's rows (issued before the MFMAs) and this wave's older
     // stores retire here; nothing younger is in flight
@@ -1841,81 +1932,11 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
         for (int jj = 0; jj < FN; ++jj) bsd[jj] = bsx[jj] = 0.f;
       }
-      if (more && !prefetch) {
-        halo_lds_barrier();
-        issue_w(jn_next);
-        issue_x(un - jn_next * a.tiles, Xn);
-        first = true;
-      }
-      continue;
-    }
-    if (a.partial && wrows > 0 && !(a.diag & 8)) {
-      // per-lane shifted sums over the fp32 accumulators of the valid rows;
-      // merged across the wave (and written) when the panel or range ends
-      ws.tile(acc, vmask);
-      if (!prefetch) {
-        float n, mean[FN], m2[FN];
-        ws.wave_merge(n, mean, m2);
-        if (lane < 16) {
+    } else {
+      if constexpr (has_add) epi_load(tile, jn, rap);
 #pragma unroll
-          for (int jj = 0; jj < FN; ++jj) {
-            const int c = jn * BN + cbase + jj * 16;
-            float* rec = a.partial + ((long)c * G * HALO_WMW + (long)g * HALO_WMW + wm) * 3;
-            rec[0] = n;
-            rec[1] = mean[jj] * n;
-            rec[2] = m2[jj];
-          }
-        }
-        ws.reset();
-      }
-    }
-    if (!(a.diag & 1)) {
-      // 16-bit stores straight from the accumulators (lane: 4 rows x 1 column
-      // per fragment; padded-grid rows go to an out-of-range offset).  Round 5
-      // measured them at 3 us of a 78 us layer-1 forward (SSIP_HALO_DIAG=1,
-      // profiles/r5_halo_lab.txt), and a transposed tile with 16-B row stores
-      // at 93 us: the 32-B pieces are not what bounds this kernel.
-      const uint32_t obase = (uint32_t)(((long)tile * rows * a.Ncols + jn * BN) * 2);
-      uint32_t off[FM][4];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) off[i][e] = obase + rowoff[i][e];
-      float bcol[FN];  // folded eval BN (FWD): per-column bias
-#pragma unroll
-      for (int jj = 0; jj < FN; ++jj) bcol[jj] = FOLD ? a.bias[jn * BN + cbase + jj * 16] : 0.f;
-      const float lo = (FOLD && a.relu) ? 0.f : -__builtin_huge_valf();
-      if (a.add) {
-        short r[FM][FN][4];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              r[i][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsA, off[i][e] + jj * 32, 0, 0);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float t = to_f32(from_f32<T>(FOLD ? acc[i][jj][e] + bcol[jj] : acc[i][jj][e])) +
-                              to_f32(__builtin_bit_cast(T, r[i][jj][e]));
-              const T o = from_f32<T>(FOLD ? fmaxf(t, lo) : t);
-              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off[i][e] + jj * 32, 0, 0);
-            }
-      } else {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < FN; ++jj)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              __builtin_amdgcn_raw_buffer_store_b16(
-                  __builtin_bit_cast(short, from_f32<T>(FOLD ? fmaxf(acc[i][jj][e] + bcol[jj], lo) : acc[i][jj][e])), rsO,
-                  off[i][e] + jj * 32, 0, 0);
-      }
+      for (int i = 0; i < FM; ++i) epi_rows(acc, i, tile, jn, rap);
+      if (stats && !prefetch) stats_flush(jn);
     }
     if (more && !prefetch) {
       // panel change: new weights and the next tile's rows, loaded once every
@@ -3243,8 +3264,12 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bp != nullptr)
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);
-  else if (bias != nullptr)  // folded eval BN epilogue
+  else if (bias != nullptr && add != nullptr)  // folded eval BN epilogue
+    hipLaunchKernelGGL((conv_halo_kernel<4, 2, true, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
+  else if (bias != nullptr)
     hipLaunchKernelGGL((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
+  else if (add != nullptr)
+    hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
   else
     hipLaunchKernelGGL((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
   return ::ssip::check_launch("conv_halo");

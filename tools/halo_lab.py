@@ -1,7 +1,7 @@
 """Layer-1 halo conv lab (GPU box): the 3x3 / stride-1 / 64-channel forward and
 dgrad of ResNet-18 layer 1 (conv_halo_kernel) at batch 256 and 128, timed
 with HIP events, per SSIP_HALO_DIAG ablation (timing only, results wrong):
-0 full, 1 no output stores, 2 no MFMAs, 4 no input-row DMA after the first
+0 full, 16 epilogue not deferred (results right), 4 no input-row DMA after the first
 tile, 8 no BN statistics (bits combine).  Speed of light per launch:
 max(FLOPs / 2.5 PF, (x + y bytes) / 8 TB/s).
 
@@ -21,7 +21,7 @@ from tune_conv import time_fn  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--diags", default="0,1,2,3,4,8,12")
+    ap.add_argument("--diags", default="0,16,4,8,12")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batches", default="256,128")
     a = ap.parse_args()

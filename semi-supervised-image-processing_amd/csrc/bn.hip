@@ -441,8 +441,16 @@ int ssip_bn_finalize(int C, int tiles, float* partial, const float* gamma, const
                    mean_out, invstd_out, scale_out, shift_out};
   const int S = fin_splits(tiles);
   double* scratch = fin_scratch(partial, (int64_t)C * tiles * 3);
-  hipLaunchKernelGGL(bn_finalize_kernel<FIN_NT>, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S,
-                     (const float*)partial, scratch, f);
+  static const bool nt64 = [] {
+    const char* e = getenv("SSIP_FIN64");  // round-5 A/B: one-wave, LDS-free finalize workgroups
+    return e != nullptr && e[0] == '1';
+  }();
+  if (nt64 && S == 1)
+    hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3(S, C), dim3(64), 0, st, C, tiles, S, (const float*)partial,
+                       scratch, f);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<FIN_NT>, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S,
+                       (const float*)partial, scratch, f);
   if (S > 1)
     hipLaunchKernelGGL(bn_finalize_merge_kernel, dim3((C + FIN_NT / 64 - 1) / (FIN_NT / 64)), dim3(FIN_NT), 0, st,
                        C, S, (const double*)scratch, f);

@@ -3,6 +3,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include "../../include/ssip.h"
+#include "stop_event.h"
 
 namespace ssip {
 static thread_local char g_err[1024] = "";
@@ -12,6 +13,11 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+}
+
+StopEvent& stop_event() {
+  static thread_local StopEvent s;
+  return s;
 }
 
 int check_launch(const char* what) {

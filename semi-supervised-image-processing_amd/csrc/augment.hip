@@ -224,7 +224,7 @@ int ssip_resize_h_u8(int B, const uint8_t* src, int64_t src_batch_stride, int Hs
   SSIP_REQUIRE(B > 0 && src && Hs > 0 && Ws > 0 && Wo > 0 && ksize > 0 && bounds && coeffs && tmp, SSIP_ERR_ARG,
                "ssip_resize_h_u8: bad arguments");
   const long total = (long)B * Hs * Wo;
-  hipLaunchKernelGGL(resize_h_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, src,
+  SSIP_KLAUNCH(resize_h_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, src,
                      (long)src_batch_stride, Hs, Ws, Wo, ksize, bounds, coeffs, tmp);
   return ::ssip::check_launch("resize_h_u8");
 }
@@ -247,7 +247,7 @@ int ssip_augment_u8(int dtype, int B, const uint8_t* src, int64_t src_batch_stri
   const dim3 grid((unsigned)((hp + rows - 1) / rows), (unsigned)B);
   const dim3 block((unsigned)(wp >= 256 ? 256 : ((wp + 63) / 64) * 64));
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(augment_kernel<T>, grid, block, 0, (hipStream_t)stream, B, src,
+    SSIP_KLAUNCH(augment_kernel<T>, grid, block, 0, (hipStream_t)stream, B, src,
                        (long)src_batch_stride, src_h, src_w, Hr, Wr, Ho, Wo, crop_x, crop_y, ksize_v, bounds_v,
                        coeffs_v, params, mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2], out_pad, rows,
                        (T*)out);
@@ -261,7 +261,7 @@ int ssip_nchw_to_nhwc(int dtype, int B, int C, int H, int W, int Cp, int out_pad
                SSIP_ERR_ARG, "ssip_nchw_to_nhwc: bad arguments");
   const long total = (long)B * (H + 2 * out_pad) * (W + 2 * out_pad) * Cp;
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, C, H, W,
+    SSIP_KLAUNCH(nchw_to_nhwc_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, C, H, W,
                        Cp, out_pad, x, (T*)out);
   });
   return ::ssip::check_launch("nchw_to_nhwc");

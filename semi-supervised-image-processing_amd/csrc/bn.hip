@@ -441,18 +441,24 @@ int ssip_bn_finalize(int C, int tiles, float* partial, const float* gamma, const
                    mean_out, invstd_out, scale_out, shift_out};
   const int S = fin_splits(tiles);
   double* scratch = fin_scratch(partial, (int64_t)C * tiles * 3);
+  // SSIP_FIN64=1: one-wave, LDS-free workgroups where one per channel
+  // suffices.  They fit beside a persistent kernel that holds a CU's whole LDS
+  // (the other stream's layer-1 halo conv), where a 256-thread workgroup with
+  // its 96-B combine waits for it to finish: layer-1 finalize 42 -> 20 us in
+  // the step trace, but the step moved -0.55 % on one box and +0.8 % on
+  // another (round 5): off by default.
   static const bool nt64 = [] {
-    const char* e = getenv("SSIP_FIN64");  // round-5 A/B: one-wave, LDS-free finalize workgroups
+    const char* e = getenv("SSIP_FIN64");
     return e != nullptr && e[0] == '1';
   }();
   if (nt64 && S == 1)
-    hipLaunchKernelGGL(bn_finalize_kernel<64>, dim3(S, C), dim3(64), 0, st, C, tiles, S, (const float*)partial,
+    SSIP_KLAUNCH(bn_finalize_kernel<64>, dim3(S, C), dim3(64), 0, st, C, tiles, S, (const float*)partial,
                        scratch, f);
   else
-    hipLaunchKernelGGL(bn_finalize_kernel<FIN_NT>, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S,
+    SSIP_KLAUNCH(bn_finalize_kernel<FIN_NT>, dim3(S, C), dim3(FIN_NT), 0, st, C, tiles, S,
                        (const float*)partial, scratch, f);
   if (S > 1)
-    hipLaunchKernelGGL(bn_finalize_merge_kernel, dim3((C + FIN_NT / 64 - 1) / (FIN_NT / 64)), dim3(FIN_NT), 0, st,
+    SSIP_KLAUNCH(bn_finalize_merge_kernel, dim3((C + FIN_NT / 64 - 1) / (FIN_NT / 64)), dim3(FIN_NT), 0, st,
                        C, S, (const double*)scratch, f);
   return ::ssip::check_launch("bn_finalize");
 }
@@ -467,7 +473,7 @@ int ssip_bn_eval_coeffs(int C, const float* gamma, const float* beta, const floa
                         float* shift_out, void* stream) {
   SSIP_REQUIRE(C > 0 && running_mean && running_var && scale_out && shift_out, SSIP_ERR_ARG,
                "ssip_bn_eval_coeffs: bad arguments");
-  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, gamma, beta,
+  SSIP_KLAUNCH(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, gamma, beta,
                      running_mean, running_var, eps, mean_out, invstd_out, scale_out, shift_out);
   return ::ssip::check_launch("bn_eval_coeffs");
 }
@@ -478,7 +484,7 @@ int ssip_bn_apply(int dtype, int64_t M, int C, const void* y, const float* scale
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply: unsupported size");
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
+    SSIP_KLAUNCH((bn_apply_kernel<T, false>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
                        total8, C, (const T*)y, scale, shift, (const T*)residual, (const float*)nullptr,
                        (const float*)nullptr, relu, (T*)z, mask_bits);
   });
@@ -493,7 +499,7 @@ int ssip_bn_apply2(int dtype, int64_t M, int C, const void* y, const float* scal
   SSIP_REQUIRE(M * C / 8 < (1l << 31) && 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_bn_apply2: unsupported size");
   const int total8 = (int)(M * C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
+    SSIP_KLAUNCH((bn_apply_kernel<T, true>), dim3(bn_elem_grid(total8)), dim3(256), 0, (hipStream_t)stream,
                        total8, C, (const T*)y, scale, shift, (const T*)y2, scale2, shift2, relu, (T*)z, mask_bits);
   });
   return ::ssip::check_launch("bn_apply2");
@@ -529,11 +535,11 @@ int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zm
   f.set[1] = bn_bwd_fin_set(pb, gamma_b, mean_b, invstd_b, dgamma_b, dbeta_b, coef + 3 * C,
                             scratch + (int64_t)C * S * 2);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_reduce_dual_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
+    SSIP_KLAUNCH(bn_bwd_reduce_dual_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, mask_bits, (const T*)ya, (const T*)yb, mean_a, invstd_a, mean_b, invstd_b, pa,
                        pb);
     launch_bn_bwd_finalize(st, C, blocks, (long)M, 1, 2, f, accumulate);
-    hipLaunchKernelGGL(bn_bwd_apply_dual_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
+    SSIP_KLAUNCH(bn_bwd_apply_dual_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
                        (const T*)dz, (const T*)zmask, mask_bits, (const T*)ya, (const T*)yb, coef, coef + 3 * C, (T*)dy_a,
                        (T*)dy_b);
   });
@@ -562,13 +568,13 @@ static int bn_bwd_impl(int dtype, int64_t M, int C, const void* dz, const void* 
   // (64-VGPR 4-channel forms that fit beside a resident wgrad made the step
   // slower, 6.70 vs 6.50 ms: r3-variants branch)
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
+    SSIP_KLAUNCH(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, (long)M, C, rows, (const T*)dz,
                        (const T*)zmask, mbits, (const T*)y, mean, invstd, mscale, mshift, partial);
     BnBwdFin f;
     f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
                               fin_scratch(partial, (int64_t)blocks * C * 2));
     launch_bn_bwd_finalize(st, C, blocks, (long)M, 1, 1, f, accumulate);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
+    SSIP_KLAUNCH(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C,
                        (const T*)dz, (const T*)zmask, mbits, (const T*)y, coef, (T*)dy, (T*)dpre, mscale, mshift);
   });
   return ::ssip::check_launch("bn_bwd");
@@ -588,7 +594,7 @@ int ssip_bn_bwd_from_partials(int dtype, int64_t M, int C, int tiles, float* par
                             fin_scratch(partial, (int64_t)tiles * C * 2));
   launch_bn_bwd_finalize(st, C, tiles, (long)M, 1, 1, f, accumulate);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
+    SSIP_KLAUNCH(bn_bwd_apply_kernel<T>, dim3(bn_elem_grid(total8)), dim3(256), 0, st, total8, C, (const T*)dout,
                        (const T*)nullptr, (const uint8_t*)nullptr, (const T*)y, coef, (T*)dy, (T*)nullptr,
                        (const float*)nullptr,
                        (const float*)nullptr);
@@ -618,7 +624,7 @@ int ssip_relu_bwd(int dtype, int64_t n, const void* g, const void* z, void* out,
   SSIP_REQUIRE(n > 0 && n % 8 == 0 && g && z && out, SSIP_ERR_ARG, "ssip_relu_bwd: bad arguments");
   const long total8 = n / 8;
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(relu_bwd_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, (hipStream_t)stream, total8,
+    SSIP_KLAUNCH(relu_bwd_kernel<T>, dim3(grid_for(total8)), dim3(256), 0, (hipStream_t)stream, total8,
                        (const T*)g, (const T*)z, (T*)out);
   });
   return ::ssip::check_launch("relu_bwd");

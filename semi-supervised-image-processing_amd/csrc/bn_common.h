@@ -134,10 +134,10 @@ __global__ void __launch_bounds__(FIN_NT) bn_bwd_finalize_merge_kernel(int C, in
 static inline void launch_bn_bwd_finalize(hipStream_t st, int C, int blocks, long M, int cmajor, int sets,
                                           const BnBwdFin& fin, int accumulate) {
   const int S = fin_splits(blocks);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel<FIN_NT>, dim3(S, sets * C), dim3(FIN_NT), 0, st, C, blocks, S, M,
+  SSIP_KLAUNCH(bn_bwd_finalize_kernel<FIN_NT>, dim3(S, sets * C), dim3(FIN_NT), 0, st, C, blocks, S, M,
                      cmajor, fin, accumulate);
   if (S > 1)
-    hipLaunchKernelGGL(bn_bwd_finalize_merge_kernel, dim3((sets * C + FIN_NT / 64 - 1) / (FIN_NT / 64)),
+    SSIP_KLAUNCH(bn_bwd_finalize_merge_kernel, dim3((sets * C + FIN_NT / 64 - 1) / (FIN_NT / 64)),
                        dim3(FIN_NT), 0, st, C, sets, S, M, fin, accumulate);
 }
 

@@ -2945,7 +2945,7 @@ template <int MODE>
 static int launch_glds(const Plan& pl, hipStream_t st) {
 #define SSIP_GLDS_GO(BM_, BN_, WM_, WN_, ST_)                                                                 \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
+    SSIP_KLAUNCH((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
                        st, pl.args);                                                                          \
     return ::ssip::check_launch("conv_glds");                                                                 \
   }
@@ -2956,7 +2956,7 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
       if (pl.args.pmean != nullptr) {  // fused BN-backward epilogue: default tiles only
 #define SSIP_GLDS_GOP(BM_, BN_, WM_, WN_, ST_)                                                                \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, true>), pl.grid,               \
+    SSIP_KLAUNCH((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, true>), pl.grid,               \
                        dim3(64 * WM_ * WN_), 0, st, pl.args);                                                 \
     return ::ssip::check_launch("conv_glds_bnpost");                                                          \
   }
@@ -2970,7 +2970,7 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
       if (pl.args.bias != nullptr) {  // folded eval BN epilogue: the default tiles only
 #define SSIP_GLDS_GOF(BM_, BN_, WM_, WN_, ST_)                                                                \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, false, true>), pl.grid,        \
+    SSIP_KLAUNCH((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, false, true>), pl.grid,        \
                        dim3(64 * WM_ * WN_), 0, st, pl.args);                                                 \
     return ::ssip::check_launch("conv_glds_fold");                                                            \
   }
@@ -2982,7 +2982,7 @@ static int launch_glds(const Plan& pl, hipStream_t st) {
       if (pl.conv1) {
 #define SSIP_GLDS_GO4(BM_, BN_, WM_, WN_, ST_)                                                                \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, true>), pl.grid, dim3(64 * WM_ * WN_), \
+    SSIP_KLAUNCH((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, true>), pl.grid, dim3(64 * WM_ * WN_), \
                        0, st, pl.args);                                                                       \
     return ::ssip::check_launch("conv_glds_stem");                                                            \
   }
@@ -3006,7 +3006,7 @@ static int launch_conv(const Plan& pl, hipStream_t st) {
   }
 #define SSIP_LAUNCH(BM_, BN_, WM_, WN_, C1_)                                                                  \
   {                                                                                                           \
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, T, BM_, BN_, WM_, WN_, C1_>), pl.grid, dim3(64 * WM_ * WN_), 0, \
+    SSIP_KLAUNCH((conv_gemm_kernel<MODE, T, BM_, BN_, WM_, WN_, C1_>), pl.grid, dim3(64 * WM_ * WN_), 0, \
                        st, pl.args);                                                                          \
   }
   const bool c1 = pl.conv1;
@@ -3183,7 +3183,7 @@ static int launch_stem_halo(const ssip_conv_desc* d, const HaloPlan& hp, const v
   s.o_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   s.N = d->N; s.H = d->H; s.W = d->W; s.P = d->P; s.Q = d->Q; s.Ncols = d->K;
   s.tiles = hp.tiles; s.units = hp.units;
-  hipLaunchKernelGGL((conv_stem_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, s);
+  SSIP_KLAUNCH((conv_stem_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, s);
   return ::ssip::check_launch("conv_stem_halo");
 }
 
@@ -3261,17 +3261,17 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   // slower in the step, where the side streams' kernels run beside them; 4
   // waves of 64x64 slower still: r3-variants branch)
   if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
-    hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bp != nullptr)
-    hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bias != nullptr && add != nullptr)  // folded eval BN epilogue
-    hipLaunchKernelGGL((conv_halo_kernel<4, 2, true, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2, true, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bias != nullptr)
-    hipLaunchKernelGGL((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
   else if (add != nullptr)
-    hipLaunchKernelGGL((conv_halo_kernel<4, 2, false, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
   return ::ssip::check_launch("conv_halo");
 }
 
@@ -3552,14 +3552,14 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
       h.dy_bytes = (uint32_t)((long)d->N * d->P * d->Q * 64 * 2);
       h.N = d->N; h.H = d->H; h.W = d->W; h.P = d->P; h.Q = d->Q; h.tiles = hp.tiles;
       hipStream_t st = (hipStream_t)stream;
-      hipLaunchKernelGGL(conv_stem_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+      SSIP_KLAUNCH(conv_stem_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
       rc = ::ssip::check_launch("conv_stem_wgrad");
       if (rc) return rc;
       const long total4 = 64L * 224 / 4;
       int lg = 0;
       while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
       const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
-      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
+      SSIP_KLAUNCH(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
                          hp.G, 64, 224, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
       return ::ssip::check_launch("wgrad_reduce");
     }
@@ -3575,14 +3575,14 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
       h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 64 * 2);
       h.N = d->N; h.H = d->H; h.W = d->W; h.TR = hp.TR; h.tiles = hp.tiles;
       hipStream_t st = (hipStream_t)stream;
-      hipLaunchKernelGGL(conv_halo_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
+      SSIP_KLAUNCH(conv_halo_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
       rc = ::ssip::check_launch("conv_halo_wgrad");
       if (rc) return rc;
       const long total4 = 64L * 576 / 4;
       int lg = 0;
       while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
       const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
-      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
+      SSIP_KLAUNCH(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
                          hp.G, 64, 576, c_real, 3, s_real, 64, 3, dw_kcrs, accumulate, lg);
       return ::ssip::check_launch("wgrad_reduce");
     }
@@ -3607,7 +3607,7 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
   const int RS = d->R * d->S;
   if (c_real == d->C && s_real == d->S && d->C % 64 == 0 && RS <= WGR_T_MAXRS && pl.args.Ng == RS * d->C &&
       pl.splits <= 32 && (long)d->K * (d->C / 64) >= 256 && (reinterpret_cast<uintptr_t>(dw_kcrs) & 15) == 0) {
-    hipLaunchKernelGGL(wgrad_reduce_t_kernel, dim3((unsigned)(d->K * (d->C / 64))), dim3(256), 0, st,
+    SSIP_KLAUNCH(wgrad_reduce_t_kernel, dim3((unsigned)(d->K * (d->C / 64))), dim3(256), 0, st,
                        (const float*)workspace, pl.splits, d->K, pl.args.Ng, d->C, RS, dw_kcrs, accumulate);
     return ::ssip::check_launch("wgrad_reduce_t");
   }
@@ -3615,7 +3615,7 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
   int lg = 0;  // split groups: double while splits allow and the grid stays within ~1024 workgroups
   while (lg < 6 && (2 << lg) <= pl.splits && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
   const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
+  SSIP_KLAUNCH(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
                      pl.splits, d->K, pl.args.Ng, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
   return ::ssip::check_launch("wgrad_reduce");
 }
@@ -3652,14 +3652,14 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
   h.ix_bytes = (uint32_t)((long)d->N * P2 * Q2 * 64);
   h.N = d->N; h.H = d->H; h.W = d->W; h.P = d->P; h.Q = d->Q; h.P2 = P2; h.Q2 = Q2; h.tiles = hp.tiles;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv_stem_bwd_wgrad2_kernel, dim3(hp.G), dim3(768), 0, st, h);
+  SSIP_KLAUNCH(conv_stem_bwd_wgrad2_kernel, dim3(hp.G), dim3(768), 0, st, h);
   int rc = ::ssip::check_launch("conv_stem_bwd_wgrad");
   if (rc) return rc;
   const long total4 = 64L * 224 / 4;
   int lg = 0;
   while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
   const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace, hp.G,
+  SSIP_KLAUNCH(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace, hp.G,
                      64, 224, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
   return ::ssip::check_launch("wgrad_reduce");
 }

@@ -12,8 +12,8 @@ constexpr int FIN_NT = 256;  // threads of a finalize workgroup
 constexpr int FIN_PT = 8;
 constexpr int FIN_SMAX = 64;
 
-// (one-wave LDS-free finalize workgroups, an A/B option in round 3, were no
-// faster: 6.52 vs 6.48 ms/step; r3-variants branch)
+// (one-wave LDS-free finalize workgroups, SSIP_FIN64=1: 6.52 vs 6.48 ms/step
+// in round 3, -0.55 % / +0.8 % on two boxes in round 5; bn.hip)
 static inline int fin_splits(long tiles) {
   long s = (tiles + (long)FIN_NT * FIN_PT - 1) / ((long)FIN_NT * FIN_PT);
   return (int)(s < 1 ? 1 : (s > FIN_SMAX ? FIN_SMAX : s));

@@ -370,7 +370,7 @@ int ssip_maxpool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pa
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   const long total = (long)N * P * Q * (C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C,
+    SSIP_KLAUNCH(maxpool_fwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C,
                        P, Q, k, s, pad, (const T*)x, (T*)y, idx);
   });
   return ::ssip::check_launch("maxpool_fwd");
@@ -383,7 +383,7 @@ int ssip_maxpool_bwd(int dtype, int N, int H, int W, int C, int k, int s, int pa
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   const long total = (long)N * H * W * (C / 8);
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C,
+    SSIP_KLAUNCH(maxpool_bwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C,
                        P, Q, k, s, pad, (const T*)dy, idx, (T*)dx);
   });
   return ::ssip::check_launch("maxpool_bwd");
@@ -395,7 +395,7 @@ int ssip_avgpool_fc_fwd(int dtype, int B, int PQ, int C, int J, const void* z, c
   SSIP_REQUIRE(!logits || (w && J > 0), SSIP_ERR_ARG, "ssip_avgpool_fc_fwd: fc weight required");
   const size_t shm = (size_t)(C + 2048) * sizeof(float);  // sfeat[C] + the group partials (<= 2048)
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(avgpool_fc_fwd_kernel<T>, dim3(B), dim3(256), shm, (hipStream_t)stream, PQ, C, J, (const T*)z,
+    SSIP_KLAUNCH(avgpool_fc_fwd_kernel<T>, dim3(B), dim3(256), shm, (hipStream_t)stream, PQ, C, J, (const T*)z,
                        w, bias, feat, logits);
   });
   return ::ssip::check_launch("avgpool_fc_fwd");
@@ -407,13 +407,13 @@ int ssip_avgpool_fc_bwd(int dtype, int B, int PQ, int C, int J, const float* dlo
   hipStream_t st = (hipStream_t)stream;
   if (dz) {
     SSIP_DISPATCH_DTYPE(dtype, T, {
-      hipLaunchKernelGGL(avgpool_fc_bwd_data_kernel<T>, dim3(B), dim3(256), 0, st, PQ, C, J, dlogits, w, (T*)dz);
+      SSIP_KLAUNCH(avgpool_fc_bwd_data_kernel<T>, dim3(B), dim3(256), 0, st, PQ, C, J, dlogits, w, (T*)dz);
     });
   }
   if (dw) {
     SSIP_REQUIRE(feat, SSIP_ERR_ARG, "ssip_avgpool_fc_bwd: feat required for dw");
     SSIP_REQUIRE(J <= 256, SSIP_ERR_ARG, "ssip_avgpool_fc_bwd: J <= 256");
-    hipLaunchKernelGGL(fc_bwd_weight_kernel, dim3((J * C + 63) / 64), dim3(1024), 0, st, B, C, J, dlogits, feat, dw,
+    SSIP_KLAUNCH(fc_bwd_weight_kernel, dim3((J * C + 63) / 64), dim3(1024), 0, st, B, C, J, dlogits, feat, dw,
                        dbias, accumulate);
   }
   return ::ssip::check_launch("avgpool_fc_bwd");
@@ -422,7 +422,7 @@ int ssip_avgpool_fc_bwd(int dtype, int B, int PQ, int C, int J, const float* dlo
 int ssip_cross_entropy(int B, int J, const float* logits, const int64_t* labels, float grad_scale, float* loss,
                        float* dlogits, int64_t* pred, void* stream) {
   SSIP_REQUIRE(B > 0 && J > 0 && J <= MAXJ && logits && labels, SSIP_ERR_ARG, "ssip_cross_entropy: bad arguments");
-  hipLaunchKernelGGL(cross_entropy_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, J, logits, labels,
+  SSIP_KLAUNCH(cross_entropy_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, J, logits, labels,
                      grad_scale, loss, dlogits, pred);
   return ::ssip::check_launch("cross_entropy");
 }
@@ -433,7 +433,7 @@ int ssip_semi_loss(int Bl, int Bu, int J, const float* zl, const int64_t* yl, co
   SSIP_REQUIRE(Bl >= 0 && Bu >= 0 && Bl + Bu > 0 && J > 0 && J <= MAXJ && out4 && (Bl == 0 || (zl && yl && dzl)) &&
                    (Bu == 0 || (zw && zs && dzs)),
                SSIP_ERR_ARG, "ssip_semi_loss: bad arguments");
-  hipLaunchKernelGGL(semi_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, Bl, Bu, J, zl, yl, zw, zs, tau,
+  SSIP_KLAUNCH(semi_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, Bl, Bu, J, zl, yl, zw, zs, tau,
                      lambda_u, out4, dzl, dzs, pseudo, mask);
   return ::ssip::check_launch("semi_loss");
 }
@@ -442,7 +442,7 @@ int ssip_softmax_select(int B, int J, const float* logits, float threshold, int 
                         int64_t* pred, uint8_t* keep, float* pos_prob, void* stream) {
   SSIP_REQUIRE(B > 0 && J > 0 && J <= MAXJ && logits && pos_col >= 0 && pos_col < J, SSIP_ERR_ARG,
                "ssip_softmax_select: bad arguments");
-  hipLaunchKernelGGL(softmax_select_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, B, J, logits,
+  SSIP_KLAUNCH(softmax_select_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, B, J, logits,
                      threshold, pos_col, probs, conf, pred, keep, pos_prob);
   return ::ssip::check_launch("softmax_select");
 }

@@ -255,14 +255,14 @@ int ssip_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float
   const float bc2_sqrt = (float)sqrt(bc2);
   long blocks = (n + 1023) / 1024;  // 4 elements per lane
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adamw_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad, exp_avg,
+  SSIP_KLAUNCH(adamw_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad, exp_avg,
                      exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, grad_scale);
   return ::ssip::check_launch("adamw");
 }
 
 int ssip_adamw_sched_step(double* sched, float beta1, float beta2, void* stream) {
   SSIP_REQUIRE(sched, SSIP_ERR_ARG, "ssip_adamw_sched_step: null schedule");
-  hipLaunchKernelGGL(adamw_sched_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sched, (double)beta1,
+  SSIP_KLAUNCH(adamw_sched_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sched, (double)beta1,
                      (double)beta2);
   return ::ssip::check_launch("adamw_sched");
 }
@@ -274,7 +274,7 @@ int ssip_adamw_dev(int64_t n, float* param, const float* grad, float* exp_avg, f
                "ssip_adamw_dev: bad arguments");
   long blocks = (n + 1023) / 1024;  // 4 elements per lane
   if (blocks > 2048) blocks = 2048;  // grid-stride: each wave computes the schedule scalars once
-  hipLaunchKernelGGL(adamw_dev_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
+  SSIP_KLAUNCH(adamw_dev_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
                      exp_avg, exp_avg_sq, sched, beta1, beta2, eps, weight_decay, grad_scale, advance ? 1 : 0);
   return ::ssip::check_launch("adamw_dev");
 }
@@ -287,7 +287,7 @@ int ssip_weight_prep(int dtype, int K, int C, int R, int S, int Cp, int Sp, cons
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(weight_prep_kernel<T>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, K, C, R, S, Cp, Sp,
+    SSIP_KLAUNCH(weight_prep_kernel<T>, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, K, C, R, S, Cp, Sp,
                        w_kcrs, (T*)w_krsc, (T*)w_crsk);
   });
   return ::ssip::check_launch("weight_prep");
@@ -315,7 +315,7 @@ extern "C" int ssip_weight_prep_batch(int dtype, int count, const ssip_wprep* it
   tab.tile_start[count] = tiles;
   tab.xcd = 1;
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(weight_prep_batch_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, tab);
+    SSIP_KLAUNCH(weight_prep_batch_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, tab);
   });
   return ::ssip::check_launch("weight_prep_batch");
 }
@@ -343,6 +343,6 @@ extern "C" int ssip_counters_add(int count, int64_t* const* ptrs, int64_t delta,
     SSIP_REQUIRE(ptrs[i], SSIP_ERR_ARG, "ssip_counters_add: null counter %d", i);
     t.p[i] = ptrs[i];
   }
-  hipLaunchKernelGGL(counters_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t, count, delta);
+  SSIP_KLAUNCH(counters_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t, count, delta);
   return ::ssip::check_launch("counters_add");
 }

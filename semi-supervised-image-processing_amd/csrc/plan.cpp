@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/ssip.h"
+#include "stop_event.h"
 
 namespace ssip {
 void set_error(const char* fmt, ...);
@@ -62,6 +63,8 @@ struct Op {
 struct ssip_plan {
   std::vector<Op> ops;
   std::vector<Op> ilv;               // ops re-ordered stream by stream (interleave_segments)
+  std::vector<int> fuse;             // per ilv op: the event an OP_CALL records as its completion, or -1
+  std::vector<int> nlaunch;          // per ilv op: launches the OP_CALL made on its stream (-1: not counted yet)
   size_t ilv_ops = (size_t)-1;       // ops.size() when ilv was built
   std::vector<uint64_t> slots;
   std::vector<std::unique_ptr<uint8_t[]>> blobs;
@@ -209,6 +212,22 @@ void interleave_segments(ssip_plan* plan) {
     }
   }
   plan->ilv_ops = plan->ops.size();
+  // an OP_CALL whose stream's next op is an event record records that event as
+  // its launches' completion (SSIP_KLAUNCH); the record op itself is then skipped
+  plan->fuse.assign(plan->ilv.size(), -1);
+  plan->nlaunch.assign(plan->ilv.size(), -1);
+  const bool off = getenv("SSIP_PLAN_MARKERS") != nullptr;  // A/B: separate marker packets
+  for (size_t i = 0; i < plan->ilv.size() && !off; ++i) {
+    const Op& op = plan->ilv[i];
+    if (op.kind != OP_CALL) continue;
+    const hipStream_t st = op_stream(plan, op);
+    for (size_t j = i + 1; j < plan->ilv.size(); ++j) {
+      const Op& nx = plan->ilv[j];
+      if (nx.kind == OP_MARK || op_stream(plan, nx) != st) continue;
+      if (nx.kind == OP_EVENT) plan->fuse[i] = (int)j;
+      break;
+    }
+  }
 }
 
 }  // namespace
@@ -224,15 +243,33 @@ int ssip_plan_run(ssip_plan* plan, int segment) {
   const size_t e = segment + 1 < (int)plan->seg_begin.size() ? plan->seg_begin[segment + 1] : plan->ops.size();
   if (plan->ilv_ops != plan->ops.size()) interleave_segments(plan);
   const std::vector<Op>& seq = plan->ilv;
+  std::vector<char> done(e - b, 0);  // event records made by the launch before them
   for (size_t i = b; i < e; ++i) {
     const Op& op = seq[i];
     switch (op.kind) {
       case OP_CALL: {
+        const int f = plan->fuse[i];
+        ::ssip::StopEvent& se = ::ssip::stop_event();
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const hipStream_t st = op_stream(plan, op);
+        if (f >= 0 && (size_t)f < e && hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+          // first replay: count the op's launches on st; later: the last one records the event
+          se.ev = plan->nlaunch[i] > 0 ? plan->events[seq[f].event] : nullptr;
+          se.st = st;
+          se.count = 0;
+          se.target = plan->nlaunch[i] > 0 ? plan->nlaunch[i] : -1;
+          se.used = 0;
+        }
         const int rc = kPlanFns[op.fn].call(plan->slots.data() + op.arg0);
+        const bool fused = se.ev != nullptr && se.used == 1 && se.count == se.target;
+        if (se.st != nullptr && plan->nlaunch[i] < 0) plan->nlaunch[i] = se.count;
+        se = ::ssip::StopEvent{};
         if (rc != SSIP_OK) return rc;  // the entry point set the message
+        if (fused) done[f - b] = 1;  // else the record op below makes it
         break;
       }
       case OP_EVENT:
+        if (done[i - b]) break;
         if (hipEventRecord(plan->events[op.event], op.stream) != hipSuccess) {
           ::ssip::set_error("ssip_plan_run: hipEventRecord failed at op %zu", i);
           return SSIP_ERR_LAUNCH;

@@ -6,6 +6,7 @@
 // (__bf16) for the throughput path.  Accumulation is always fp32.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 #include "../../include/ssip.h"
@@ -22,7 +23,23 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;
 namespace ssip {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+
 }  // namespace ssip
+#include "stop_event.h"
+
+// Every kernel launch of the library goes through this (hipLaunchKernelGGL's
+// arguments).
+#define SSIP_KLAUNCH(kernel, grid, block, shm, stream, ...)                                            \
+  do {                                                                                                 \
+    ::ssip::StopEvent& se_ = ::ssip::stop_event();                                                     \
+    if (se_.st != nullptr && (hipStream_t)(stream) == se_.st && ++se_.count == se_.target &&           \
+        se_.ev != nullptr) {                                                                           \
+      hipExtLaunchKernelGGL(kernel, grid, block, shm, stream, nullptr, se_.ev, 0, __VA_ARGS__);        \
+      ++se_.used;                                                                                      \
+    } else {                                                                                           \
+      hipLaunchKernelGGL(kernel, grid, block, shm, stream, __VA_ARGS__);                               \
+    }                                                                                                  \
+  } while (0)
 
 #define SSIP_REQUIRE(cond, code, ...)        \
   do {                                       \

@@ -307,7 +307,7 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   SSIP_REQUIRE((long)N * H * W * C < (1l << 31), SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: too large");
   SSIP_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(stem_bn_pool_fwd_kernel<T>, dim3(N * P), dim3(256), 0, (hipStream_t)stream, H, W, C, P, Q,
+    SSIP_KLAUNCH(stem_bn_pool_fwd_kernel<T>, dim3(N * P), dim3(256), 0, (hipStream_t)stream, H, W, C, P, Q,
                        k, s, pad, (const T*)y, scale, shift, (T*)out, idx, (T*)ymax);
   });
   return ::ssip::check_launch("stem_bn_pool_fwd");
@@ -348,18 +348,18 @@ int ssip_stem_pool_bn_bwd(int dtype, int N, int H, int W, int C, int k, int s, i
   SSIP_REQUIRE(!ymax || 256 % (C / 8) == 0, SSIP_ERR_ARG, "ssip_stem_pool_bn_bwd: unsupported C");
   SSIP_DISPATCH_DTYPE(dtype, T, {
     if (ymax)
-      hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(red_blocks), dim3(256), 0, st, Mp, C, prow, (const T*)dpool,
+      SSIP_KLAUNCH(bn_bwd_reduce_kernel<T>, dim3(red_blocks), dim3(256), 0, st, Mp, C, prow, (const T*)dpool,
                          (const T*)nullptr, (const uint8_t*)nullptr, (const T*)ymax, mean, invstd, scale, shift,
                          partial);
     else
-      hipLaunchKernelGGL(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
+      SSIP_KLAUNCH(stem_pool_bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(128), 0, st, N, H, W, C, P, Q, k, s,
                          pad, rows, (const T*)dpool, idx, (const T*)y, scale, shift, mean, invstd, partial);
     BnBwdFin f;
     f.set[0] = bn_bwd_fin_set(partial, gamma, mean, invstd, dgamma, dbeta, coef,
                               fin_scratch(partial, (int64_t)red_blocks * C * 2));
     launch_bn_bwd_finalize(st, C, red_blocks, M, 1, 1, f, accumulate);
     if (dy)  // dy == nullptr: only dgamma/dbeta/coef (ssip_stem_bwd_wgrad forms dy on the fly)
-      hipLaunchKernelGGL(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
+      SSIP_KLAUNCH(stem_pool_bn_bwd_apply_kernel<T>, dim3(N * H), dim3(128), 0, st, H, W, C, P, Q, k, s, pad,
                          (const T*)dpool, idx, (const T*)y, scale, shift, coef, (T*)dy);
   });
   return ::ssip::check_launch("stem_pool_bn_bwd");

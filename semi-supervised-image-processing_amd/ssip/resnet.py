@@ -647,10 +647,6 @@ WGRAD_SIDE_STREAM = os.environ.get("SSIP_WGRAD_STREAM", "1") != "0"
 # measurement only (bench.py's production roofline leg): keep the side
 # stream's wgrad grid budgets when everything runs serialised on one stream
 WGRAD_BUDGET_SERIAL = False
-# One main->side event per block instead of one per wgrad (SSIP_WGRAD_BATCH=0:
-# per wgrad).  Every event record on the main stream sat as a ~6.5 us bubble
-# before the next dgrad in the round-5 step trace (16 per step).
-_WGRAD_BATCH = os.environ.get("SSIP_WGRAD_BATCH", "1") != "0"
 _side_streams = {}
 
 
@@ -856,22 +852,6 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                         partial, coef_buf[: 6 * g.K], mbits)
         return dya, dyb
 
-    wg_queue = []  # side-stream wgrads of the current block, enqueued behind one event
-    batch_off = False  # the last two blocks (layer 1) keep one event per wgrad: their wgrads
-    # and the stem's are the step's tail, and holding them to the block end lengthens it
-
-    def flush_wgrads():
-        if not wg_queue:
-            return
-        ops.wait_stream(side, main)
-        with torch.cuda.stream(side):
-            for rec, dy, tgt, acc in wg_queue:
-                ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
-                               max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev))
-        for rec, dy, _, _ in wg_queue:
-            dy.record_stream(side)
-        wg_queue.clear()
-
     def conv_wgrad(rec: _ConvRec, dy):
         w = rec.conv.weight
         if not w.requires_grad:
@@ -881,9 +861,14 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
             ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
                            max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev) if WGRAD_BUDGET_SERIAL else 0)
             return
-        wg_queue.append((rec, dy, tgt, acc))
-        if not _WGRAD_BATCH or batch_off:
-            flush_wgrads()
+        # (round 5: holding a block's wgrads behind one event at its end -- 8
+        # event records instead of 19 -- made the step 3 % slower: the side
+        # stream idles while they wait)
+        ops.wait_stream(side, main)
+        with torch.cuda.stream(side):
+            ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
+                           max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev))
+        dy.record_stream(side)
 
     def conv_dgrad(rec: _ConvRec, dy, out, add=None):
         crsk = _prepped_t(model, rec)[1]
@@ -914,7 +899,6 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
     pending = None  # (dpre, partial, tiles) of the current block's last BN, from the block above
     for bi in range(nblocks - 1, -1, -1):
         recs, ds, xin = sv.blocks[bi]
-        batch_off = bi < 2
         stage_idx = bi + 1
         need_dx = first_trainable is not None and first_trainable < stage_idx
         below = sv.blocks[bi - 1][0][-1] if bi > 0 else None  # BN+ReLU producing this block's input
@@ -969,8 +953,6 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                     pending = conv_dgrad_bn(ds, dy_ds, below, dxin, dxin, residual=True)
                 else:
                     conv_dgrad(ds, dy_ds, dxin, dxin)
-        if side is not None:
-            flush_wgrads()
         if hook is not None:
             hook(list(blocks[bi].parameters()))
         dz = dxin

@@ -1579,7 +1579,8 @@ struct HaloArgs {
   const float *pmean, *pinvstd, *pmscale, *pmshift;
   uint32_t bits_bytes;
   int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 4 no input-row DMA after the
-             // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt)
+             // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt);
+             // 16 (results right): the next tile's rows issued before the MFMAs, not among them
 };
 
 constexpr int HALO_XBUF = 44 * 1024;
@@ -1694,19 +1695,22 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   const int rows = a.TR * a.W;     // output pixels per tile
   const int mrows = a.TR * Wp;     // GEMM rows per tile: the padded grid (q = W, W+1 are discarded)
 
+  // one 1-KiB LDS-DMA piece (8 pixels) of tile (n, p0)'s input rows
+  auto issue_x_piece = [&](int n, int p0, int i, char* Xs) {
+    const int px = i * 8 + (lane >> 3);
+    const int sr = px / Wp, sc = px - sr * Wp;
+    const int pin = p0 - 1 + sr, win = sc - 1;
+    const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
+    const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
+    const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
+    blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
+  };
   auto issue_x = [&](int tile, char* Xs) {
     const int R0 = tile * a.TR;
     const int n = R0 / a.H, p0 = R0 - n * a.H;
-    for (int i = wave; i < nxi; i += NW) {
-      const int px = i * 8 + (lane >> 3);
-      const int sr = px / Wp, sc = px - sr * Wp;
-      const int pin = p0 - 1 + sr, win = sc - 1;
-      const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
-      const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
-      const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
-      blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
-    }
+    for (int i = wave; i < nxi; i += NW) issue_x_piece(n, p0, i, Xs);
   };
+  constexpr int XPW = (HALO_XBUF / 1024 + NW - 1) / NW;  // most pieces per wave and tile
   auto issue_w = [&](int jn) {
     for (int i = wave; i < 72; i += NW) {
       const int tw = i >> 3, col = ((i & 7) << 3) + (lane >> 3);
@@ -1862,7 +1866,14 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     const bool more = un < u1;
     const int jn_next = more ? un / a.tiles : jn;
     const bool prefetch = more && jn_next == jn;
-    if (prefetch && !(a.diag & 4)) issue_x(un - jn * a.tiles, Xn);  // tile u-1's buffer: every wave is past its reads
+    // the next tile's rows go to tile u-1's buffer (every wave is past its
+    // reads): one piece per wave after every other k-step's MFMAs, so the
+    // DMA issue (~60-185 cycles a piece) runs beside the matrix pipe instead
+    // of ahead of it with the partner wave's in the same place
+    const bool spread = prefetch && !(a.diag & 4) && !(a.diag & 16);
+    const int nR0 = (un - jn * a.tiles) * a.TR;
+    const int nn = nR0 / a.H, np0 = nR0 - nn * a.H;
+    if (prefetch && !(a.diag & 4) && (a.diag & 16)) issue_x(un - jn * a.tiles, Xn);
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -1901,6 +1912,10 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
+      if (st % 2 == 0 && st / 2 < XPW) {
+        const int i = wave + (st / 2) * NW;
+        if (spread && i < nxi) issue_x_piece(nn, np0, i, Xn);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     // the next tile's rows (issued before the MFMAs) and this wave's older
@@ -2191,10 +2206,12 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
   const int Wp = a.W + 2;
   const int npx = (a.TR + 2) * Wp, mrows = a.TR * Wp;
 
-  auto issue = [&](int tile, char* Xs, char* Ds) {
-    const int R0 = tile * a.TR;
-    const int n = R0 / a.H, p0 = R0 - n * a.H;
-    for (int i = wave; i < HWG_XBUF / 1024; i += NW) {  // input image: 8 rows per instruction
+  // LDS-DMA pieces of a tile: all 48 of the input image's (the k-loop reads
+  // rows up to 255 + 2 Wp + 2: dy is zero at m >= mrows, but 0 x garbage in
+  // an unfilled row is NaN), then all 32 of dy's
+  constexpr int nxp = HWG_XBUF / 1024, npieces = nxp + HWG_DBUF / 1024;
+  auto issue_piece = [&](int n, int p0, int i, char* Xs, char* Ds) {
+    if (i < nxp) {  // input image: 8 rows per instruction
       const int px = i * 8 + (lane >> 3);
       const int sr = px / Wp, sc = px - sr * Wp;
       const int pin = p0 - 1 + sr, win = sc - 1;
@@ -2202,15 +2219,19 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
       const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
       const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
       blds16(rsX, ok ? off : SSIP_OOB, Xs + i * 1024);
-    }
-    for (int i = wave; i < HWG_DBUF / 1024; i += NW) {  // dy rows of the padded grid
-      const int m = i * 8 + (lane >> 3);
+    } else {  // dy rows of the padded grid
+      const int m = (i - nxp) * 8 + (lane >> 3);
       const int j = m / Wp, q = m - j * Wp;
       const int ch = (lane & 7) ^ mt64_chunk_xor(m);
       const bool ok = m < mrows && q < a.W;
       const uint32_t off = (uint32_t)(((((long)n * a.H + p0 + j) * a.W + q) * 64 + ch * 8) * 2);
-      blds16(rsD, ok ? off : SSIP_OOB, Ds + i * 1024);
+      blds16(rsD, ok ? off : SSIP_OOB, Ds + (i - nxp) * 1024);
     }
+  };
+  auto issue = [&](int tile, char* Xs, char* Ds) {
+    const int R0 = tile * a.TR;
+    const int n = R0 / a.H, p0 = R0 - n * a.H;
+    for (int i = wave; i < npieces; i += NW) issue_piece(n, p0, i, Xs, Ds);
   };
 
   f32x4 acc[2][9];
@@ -2254,6 +2275,8 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
     if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     first = false;
     halo_lds_barrier();
+    // (round 5: issuing these pieces among the k-steps' MFMAs instead, as
+    // conv_halo_kernel does, pushed this kernel past 256 VGPRs into spills)
     if (u + 1 < u1) issue(u + 1, Xn, Xn + HWG_XBUF);
     Frag<T> fa[2][2], fb[2][9];
     auto load_step = [&](int ks, Frag<T>(&ra)[2], Frag<T>(&rb)[9]) {

@@ -1608,7 +1608,8 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
                                                      __amdgpu_buffer_rsrc_t rsO, __amdgpu_buffer_rsrc_t rsA,
                                                      __amdgpu_buffer_rsrc_t rsY, __amdgpu_buffer_rsrc_t rsM, int tile,
                                                      int rows, int col0, const uint32_t (&rowoff)[FM][4],
-                                                     uint32_t vmask, int cbase, float (&bsd)[FN], float (&bsx)[FN]) {
+                                                     uint32_t vmask, int cbase, float (&bsd)[FN], float (&bsx)[FN],
+                                                     const short (*pre_y)[FN][4] = nullptr) {
   typedef __bf16 T;
   static_assert(FM % BATCH == 0, "row-group batches");
   const uint32_t obase = (uint32_t)(((long)tile * rows * a.Ncols + col0) * 2);
@@ -1639,7 +1640,7 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
           const int i = i0 + b;
           const uint32_t off = obase + rowoff[i][e] + jj * 32;
           const bool valid = (vmask >> (i * 4 + e)) & 1u;
-          ry[b][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsY, off, 0, 0);
+          ry[b][jj][e] = pre_y ? pre_y[i][jj][e] : __builtin_amdgcn_raw_buffer_load_b16(rsY, off, 0, 0);
           ra[b][jj][e] = has_add ? __builtin_amdgcn_raw_buffer_load_b16(rsA, off, 0, 0) : (short)0;
           rm[b][jj][e] =
               bits ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsM, valid ? off >> 4 : SSIP_OOB, 0, 0) : 0u;
@@ -1866,6 +1867,20 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     const bool more = un < u1;
     const int jn_next = more ? un / a.tiles : jn;
     const bool prefetch = more && jn_next == jn;
+    // this tile's epilogue operands (the residual; BNPOST 1: y) are requested
+    // now and land during the MFMAs: loaded after them, each tile paid a
+    // dependent HBM round trip before its stores
+    if constexpr (BNPOST == 0 && has_add) epi_load(tile, jn, rap);
+    if constexpr (BNPOST == 1) {
+      const uint32_t ob = (uint32_t)(((long)tile * rows * a.Ncols + jn * BN) * 2);  // the epilogue's obase
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            rap[i][jj][e] = __builtin_amdgcn_raw_buffer_load_b16(rsY, ob + rowoff[i][e] + jj * 32, 0, 0);
+    }
     // the next tile's rows go to tile u-1's buffer (every wave is past its
     // reads): one piece per wave after every other k-step's MFMAs, so the
     // DMA issue (~60-185 cycles a piece) runs beside the matrix pipe instead
@@ -1924,8 +1939,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 
     // ---- epilogue
     if constexpr (BNPOST) {
-      halo_bnpost_epilogue<FM, FN, BNPOST == 1 ? FM : 1, BNPOST == 1>(a, acc, rsO, rsA, rsY, rsM, tile, rows,
-                                                                          jn * BN, rowoff, vmask, cbase, bsd, bsx);
+      halo_bnpost_epilogue<FM, FN, BNPOST == 1 ? FM : 1, BNPOST == 1>(
+          a, acc, rsO, rsA, rsY, rsM, tile, rows, jn * BN, rowoff, vmask, cbase, bsd, bsx,
+          BNPOST == 1 ? rap : nullptr);
       if (!prefetch) {
         // panel / range end: the wave's column sums -> records [c][g][wm]
 #pragma unroll
@@ -1948,7 +1964,6 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
         for (int jj = 0; jj < FN; ++jj) bsd[jj] = bsx[jj] = 0.f;
       }
     } else {
-      if constexpr (has_add) epi_load(tile, jn, rap);
 #pragma unroll
       for (int i = 0; i < FM; ++i) epi_rows(acc, i, tile, jn, rap);
       if (stats && !prefetch) stats_flush(jn);

@@ -45,6 +45,17 @@ def main():
             print(f"  diag {dg}: fwd {tf:6.1f} us ({sol / tf:.2f} SoL, {g.flops() / tf / 1e6:4.0f} TF/s)"
                   f"  dgrad {td:6.1f} us ({sol / td:.2f} SoL)", flush=True)
         os.environ.pop("SSIP_HALO_DIAG", None)
+        # the step's other two dgrad forms: + residual gradient, and the fused
+        # BN-backward reduction of the BN+ReLU below (mask from its affine)
+        add = torch.randn_like(dx)
+        yb = torch.randn_like(dx)
+        mean, inv = torch.randn(64, device=dev) * 0.1, torch.rand(64, device=dev) + 0.5
+        msc, msh = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev) * 0.1
+        dpart = torch.empty(ops.conv_dgrad_bn_partial_floats(g), device=dev)
+        ta = time_fn(lambda: ops.conv_dgrad(g, y, wc, dx, add), a.iters)
+        tb = time_fn(lambda: ops.conv_dgrad_bn(g, y, wc, None, None, yb, mean, inv, dx, dpart, mscale=msc,
+                                                mshift=msh), a.iters)
+        print(f"  dgrad + residual {ta:6.1f} us   dgrad + BN-backward reduce (affine mask) {tb:6.1f} us", flush=True)
         # the stem conv (conv_stem_halo_kernel): pre-padded 230x230x4 image, 7x7/2 -> 112x112x64
         gs = ops.ConvGeom(n, 230, 230, 4, 64, 7, 8, 2, 0, 3, 7)
         xs = torch.randn(n, 230, 230, 4, device=dev).to(bf)

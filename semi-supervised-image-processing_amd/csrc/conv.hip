@@ -2190,6 +2190,7 @@ struct HaloWgArgs {
   float* slab;       // [G][64][576]
   uint32_t x_bytes;
   int N, H, W, TR, tiles;
+  int spread;        // the next tile's pieces among the k-steps' MFMAs (SSIP_HWG_SPREAD=0: ahead of them)
 };
 
 constexpr int HWG_XBUF = 48 * 1024;  // 384 input-image rows x 128 B
@@ -2211,7 +2212,12 @@ __device__ __forceinline__ void read_tfrag(Frag<__bf16>& f, const char* base, in
 __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArgs a) {
   typedef __bf16 T;
   constexpr int NW = 8;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (HWG_XBUF + HWG_DBUF)];
+  // the two tile buffers as two objects: the tile loop runs unrolled by two,
+  // so the compiler sees that this tile's fragment reads and the next tile's
+  // LDS-DMA never alias (one array: a vmcnt(0) wait for the DMA ahead of every
+  // read that followed it)
+  __shared__ __attribute__((aligned(16))) char smem0[HWG_XBUF + HWG_DBUF];
+  __shared__ __attribute__((aligned(16))) char smem1[HWG_XBUF + HWG_DBUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // k rows 32 wm .. +31; column blocks 9 wn .. 9 wn + 8
@@ -2248,6 +2254,43 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
     const int n = R0 / a.H, p0 = R0 - n * a.H;
     for (int i = wave; i < npieces; i += NW) issue_piece(n, p0, i, Xs, Ds);
   };
+  // This wave's pieces of every tile -- i = wave + 8 k: k < 6 input image, k >= 6
+  // dy -- as tile-independent byte offsets from the tile's first pixel, with
+  // the input piece's row (0 .. TR + 1) in bits 0-2 and bit 3 set where the
+  // piece lane is always out of range; only the input rows above / below the
+  // image depend on the tile.  The k-loop issues them two per k-step, beside
+  // the MFMAs, without the division of issue_piece.
+  static_assert(nxp == 6 * NW && npieces == 10 * NW, "piece map");
+  int pc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    if (k < 6) {
+      const int px = (wave + NW * k) * 8 + (lane >> 3);
+      const int sr = px / Wp, sc = px - sr * Wp, win = sc - 1;
+      const int ch = (lane & 7) ^ mt64_chunk_xor(px);
+      const bool ok = px < npx && win >= 0 && win < a.W;
+      pc[k] = ((((sr - 1) * a.W + win) * 64 + ch * 8) * 2) | (sr & 7) | (ok ? 0 : 8);
+    } else {
+      const int m = (wave + NW * (k - 6)) * 8 + (lane >> 3);
+      const int j = m / Wp, q = m - j * Wp;
+      const int ch = (lane & 7) ^ mt64_chunk_xor(m);
+      const bool ok = m < mrows && q < a.W;
+      pc[k] = (((j * a.W + q) * 64 + ch * 8) * 2) | (ok ? 0 : 8);
+    }
+  }
+  auto issue_pc = [&](int k, int base, int p0, char* Xs, char* Ds) {
+    const int v = pc[k];
+    bool ok = (v & 8) == 0;
+    if (k < 6) {
+      const int pin = p0 - 1 + (v & 7);
+      ok = ok && pin >= 0 && pin < a.H;
+    }
+    const uint32_t off = (uint32_t)(base + (v & ~15));
+    if (k < 6)
+      blds16(rsX, ok ? off : SSIP_OOB, Xs + (wave + NW * k) * 1024);
+    else
+      blds16(rsD, ok ? off : SSIP_OOB, Ds + (wave + NW * (k - 6)) * 1024);
+  };
 
   f32x4 acc[2][9];
 #pragma unroll
@@ -2281,18 +2324,20 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
     f.v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   };
 
-  if (u0 < u1) issue(u0, smem, smem + HWG_XBUF);
-  bool first = true;
-  for (int u = u0; u < u1; ++u) {
-    char* const Xs = smem + ((u - u0) & 1) * (HWG_XBUF + HWG_DBUF);
+  if (u0 < u1) issue(u0, smem0, smem0 + HWG_XBUF);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  auto run_tile = [&](int u, char* const Xs, char* const Xn) {
     char* const Ds = Xs + HWG_XBUF;
-    char* const Xn = smem + ((u - u0 + 1) & 1) * (HWG_XBUF + HWG_DBUF);
-    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    first = false;
     halo_lds_barrier();
-    // (round 5: issuing these pieces among the k-steps' MFMAs instead, as
-    // conv_halo_kernel does, pushed this kernel past 256 VGPRs into spills)
-    if (u + 1 < u1) issue(u + 1, Xn, Xn + HWG_XBUF);
+    // the next tile's pieces: two per wave after each of k-steps 0-4's MFMAs
+    // (beside the matrix pipe instead of ahead of it, where both waves of a
+    // SIMD issued theirs at once; SSIP_HWG_SPREAD=0: ahead, as before)
+    const bool nxt = u + 1 < u1;
+    if (nxt && !a.spread) issue(u + 1, Xn, Xn + HWG_XBUF);
+    const int nR0 = (u + 1) * a.TR;
+    const int nn = nR0 / a.H, np0 = nR0 - nn * a.H;
+    const int nbase = (nn * a.H + np0) * a.W * 128;
+    const bool spread = nxt && a.spread;
     Frag<T> fa[2][2], fb[2][9];
     auto load_step = [&](int ks, Frag<T>(&ra)[2], Frag<T>(&rb)[9]) {
 #pragma unroll
@@ -2308,8 +2353,16 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
       for (int x = 0; x < 2; ++x)
 #pragma unroll
         for (int b = 0; b < 9; ++b) mma(acc[x][b], fa[ks & 1][x], fb[ks & 1][b]);
+      if (ks < 5 && spread) {
+        issue_pc(2 * ks, nbase, np0, Xn, Xn + HWG_XBUF);
+        issue_pc(2 * ks + 1, nbase, np0, Xn, Xn + HWG_XBUF);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's rows land before the barrier
+  };
+  for (int u = u0; u < u1; u += 2) {
+    run_tile(u, smem0, smem1);
+    if (u + 1 < u1) run_tile(u + 1, smem1, smem0);
   }
   // this workgroup's partial dW: slab[g][k][(t, c)]
   float* sl = a.slab + (long)g * 64 * 576;
@@ -3612,6 +3665,11 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
       h.slab = static_cast<float*>(workspace);
       h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 64 * 2);
       h.N = d->N; h.H = d->H; h.W = d->W; h.TR = hp.TR; h.tiles = hp.tiles;
+      static const int spread = [] {
+        const char* e = getenv("SSIP_HWG_SPREAD");
+        return (e != nullptr && e[0] == '0') ? 0 : 1;
+      }();
+      h.spread = spread;
       hipStream_t st = (hipStream_t)stream;
       SSIP_KLAUNCH(conv_halo_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
       rc = ::ssip::check_launch("conv_halo_wgrad");

@@ -664,6 +664,9 @@ def _cu_count(dev: torch.device) -> int:
 _side_budgets = {}
 
 
+_HALO_WG_FRAC = float(os.environ.get("SSIP_HALO_WG_FRAC", "0.5"))  # share of the CUs for the layer-1 wgrad
+
+
 def _side_wgrad_budget(g, dtype, dev: torch.device) -> int:
     """Grid cap of a wgrad on the side stream, beside the main stream's dgrad /
     BN-backward chain (ssip_conv_wgrad_budget): the split-K LDS-DMA wgrads one
@@ -676,7 +679,8 @@ def _side_wgrad_budget(g, dtype, dev: torch.device) -> int:
     b = _side_budgets.get(key)
     if b is None:
         cus = _cu_count(dev)
-        b = _side_budgets[key] = cus // 2 if ops.conv_kernel_name("wgrad", g, dtype).startswith("halo_wgrad") else cus
+        halo = ops.conv_kernel_name("wgrad", g, dtype).startswith("halo_wgrad")
+        b = _side_budgets[key] = int(cus * _HALO_WG_FRAC) if halo else cus
     return b
 
 

@@ -106,6 +106,7 @@ struct ConvArgs {
   uint32_t a2_bytes, b2_bytes;
   int ds_from;
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
+  int dma_mid;  // LDS-DMA ring: the next stage's pieces after the k-step's reads, before its second MFMA half (SSIP_DMA_MID)
   // FWD of a 3x3 / stride-s conv fused with its block's 1x1 / stride-s
   // downsample (ssip_conv_fwd_ds): workgroups >= fwd_tiles1 compute the
   // downsample's tiles -- its input pixel is the conv's tap (1, 1) pixel, so
@@ -1307,7 +1308,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   Frag<T> fa[2][FM], fb[2][FN];
   for (int ks = 0; ks < nsteps; ++ks) {
     if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
-    if (ks + NSTAGE - 1 < nsteps) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
+    const bool refill = ks + NSTAGE - 1 < nsteps;
+    if (refill && !a.dma_mid) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
     const char* As = smem + stage * STAGE;
     const char* Bs = As + A_BYTES;
     // both k-halves' fragments are requested before the first MFMA, so the
@@ -1344,6 +1346,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
           for (int j = 0; j < FN; ++j) read_mfrag<BN>(fb[1][j], Bs, wn * WTN + j * 16, lane, 1);
         }
       }
+      // (dma_mid: after every fragment read of the step, so no read follows
+      // the DMA into the ring before the next step's barrier)
+      if (h == 1 && refill && a.dma_mid) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -3002,6 +3007,14 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   const int tiles_m = ceil_div(a.M, pl.bm);
   pl.grid = dim3(tiles_m * a.tiles_n, pl.splits, 1);
   a.xcd_remap = 1;
+  {
+    // SSIP_DMA_MID: 0 never, 1 every LDS-DMA ring, 2 the 256x256 tiles only
+    static const int mid = [] {
+      const char* e = getenv("SSIP_DMA_MID");
+      return e != nullptr ? atoi(e) : 0;
+    }();
+    a.dma_mid = mid == 1 || (mid == 2 && pl.bm == 256 && pl.bn == 256);
+  }
   return SSIP_OK;
 }
 

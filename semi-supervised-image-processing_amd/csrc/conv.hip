@@ -2005,6 +2005,7 @@ struct StemArgs {
   float* partial;     // BN records (nullable)
   uint32_t x_bytes, w_bytes, o_bytes;
   int N, H, W, P, Q, Ncols, tiles, units;
+  int diag;  // timing ablations only (SSIP_STEM_DIAG, results wrong): 1 no output stores, 8 no BN statistics
 };
 
 constexpr int STEM_QP = 128, STEM_TR = 2, STEM_XROWS = 2 * STEM_TR + 5;
@@ -2136,7 +2137,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    if (a.partial && wrows > 0) {
+    if (a.partial && wrows > 0 && !(a.diag & 8)) {
       // per-lane shifted sums over the fp32 accumulators of the valid rows;
       // merged across the wave (and written) when the panel or range ends
       ws.tile(acc, vmask);
@@ -2156,7 +2157,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 2) conv_stem_hal
         ws.reset();
       }
     }
-    {
+    if (!(a.diag & 1)) {
       const uint32_t obase = (uint32_t)(((long)tile * STEM_TR * a.Q * a.Ncols + jn * BN) * 2);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -3287,6 +3288,8 @@ static int launch_stem_halo(const ssip_conv_desc* d, const HaloPlan& hp, const v
   s.o_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   s.N = d->N; s.H = d->H; s.W = d->W; s.P = d->P; s.Q = d->Q; s.Ncols = d->K;
   s.tiles = hp.tiles; s.units = hp.units;
+  s.diag = 0;
+  if (const char* dg = getenv("SSIP_STEM_DIAG")) s.diag = atoi(dg);
   SSIP_KLAUNCH((conv_stem_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, s);
   return ::ssip::check_launch("conv_stem_halo");
 }

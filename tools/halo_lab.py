@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--diags", default="0,16,4,8,12")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--stem-diags", default="0", help="SSIP_STEM_DIAG values: 1 no stores, 8 no BN statistics")
     ap.add_argument("--batches", default="256,128")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -62,9 +63,12 @@ def main():
         ws_ = (torch.randn(64, 7, 8, 4, device=dev) * 0.05).to(bf)
         ys = torch.empty(n, 112, 112, 64, device=dev, dtype=bf)
         ssol = max(gs.flops() / 2.5e15, (xs.numel() + ys.numel()) * 2 / 8e12) * 1e6
-        t = time_fn(lambda: ops.conv_fwd(gs, xs, ws_, ys, part), a.iters)
-        print(f"  stem {ops.conv_kernel_name('fwd', gs, bf)}: {t:6.1f} us ({ssol / t:.2f} of SoL "
-              f"{ssol:.1f} us)", flush=True)
+        for sd in a.stem_diags.split(","):
+            os.environ["SSIP_STEM_DIAG"] = sd
+            t = time_fn(lambda: ops.conv_fwd(gs, xs, ws_, ys, part), a.iters)
+            print(f"  stem {ops.conv_kernel_name('fwd', gs, bf)} diag {sd}: {t:6.1f} us ({ssol / t:.2f} of SoL "
+                  f"{ssol:.1f} us)", flush=True)
+        os.environ.pop("SSIP_STEM_DIAG", None)
         sc = torch.rand(64, device=dev) + 0.5
         sh = torch.randn(64, device=dev) * 0.1
         pool = torch.empty(n, 56, 56, 64, device=dev, dtype=bf)

@@ -2949,6 +2949,9 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   // l2.3x3 110.9 -> 89.1 us with 128x256, l3.3x3 109.9 -> 73.9 and l4.3x3
   // 101.4 -> 75.4 with 256x256) -- but not in the step (wgrad_big_mode)
   const int bigm = mode == MODE_WGRAD ? wgrad_big_mode() : 0;
+  // (round 5 also measured 8-wave 128x256 tiles at the budget -- two waves
+  // per SIMD, 96 KiB of LDS, so not the whole CU: 517.6 -> 461.1 us over the
+  // six layer 2-4 wgrads, but the step 6.14 -> 6.43 ms, 4 + 4 runs)
   if (mode == MODE_WGRAD && wg_budget > 0 && pl.stages > 0 && !pl.conv1 && bigm > 0) {
     // (the 1x1 downsample wgrads, Ng <= 256, keep their many-tile grids)
     if (a.M % 256 == 0 && a.Ng % 256 == 0 && a.Ng >= 512) {

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 12
+#define SSIP_ABI_VERSION 13
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -148,6 +148,21 @@ int64_t ssip_conv_wgrad_workspace_bytes_budget(const ssip_conv_desc* d, int max_
 int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, const void* x, float* dw_kcrs,
                            int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
                            int max_workgroups, void* stream);
+
+/* ABI 13: a conv whose input is the ReLU(BatchNorm) of the layer below,
+ * formed in the conv's LDS tile instead of a separate apply pass:
+ *   x = relu(fma(y_in, in_scale[c], in_shift[c]))   (ssip_bn_apply's arithmetic)
+ * Replaces the bn1 -> relu -> conv2 sequence of a torchvision BasicBlock /
+ * Bottleneck (model(inputs) at src/training/common.py:380) where conv2 is the
+ * layer-1 3x3 / stride 1 / pad 1, 64 -> 64 conv (the halo kernels); the
+ * weight gradient of the same conv takes the same input.  Bit-identical to
+ * ssip_bn_apply followed by ssip_conv_fwd / ssip_conv_wgrad. */
+int ssip_conv_bnrelu_in_supported(const ssip_conv_desc* d, int dtype);
+int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in, const float* in_scale,
+                            const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* stream);
+int ssip_conv_wgrad_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* dy, const void* y_in,
+                              const float* in_scale, const float* in_shift, float* dw_kcrs, int accumulate,
+                              void* workspace, int64_t workspace_bytes, int max_workgroups, void* stream);
 
 /* Name of the kernel a pass selects for this geometry (mode 0 = fwd,
  * 1 = dgrad, 2 = wgrad), e.g. "glds<fwd,256x256,4x2,2,splits=1>" or

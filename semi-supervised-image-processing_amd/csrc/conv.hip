@@ -1583,6 +1583,9 @@ struct HaloArgs {
   const uint8_t* pbits;
   const float *pmean, *pinvstd, *pmscale, *pmshift;
   uint32_t bits_bytes;
+  // INBN (FWD): the input is y of the BN+ReLU below; x = relu(fma(y, in_scale,
+  // in_shift)) is formed in LDS (ssip_conv_fwd_bnrelu_in)
+  const float *in_scale, *in_shift;
   int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 4 no input-row DMA after the
              // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt);
              // 16 (results right): the next tile's rows issued before the MFMAs, not among them
@@ -1676,7 +1679,24 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
 // mask from the BN affine (y is the only extra operand: one load batch per
 // tile); 2 = any other post-op operand set (one load batch per row group:
 // the registers hold no more without spilling)
-template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool ADD = false>
+// relu(fma(v, scale, shift)) over the 8 channels c0 .. c0 + 7 of one LDS
+// chunk, in place -- bn_apply_kernel's arithmetic exactly, so a conv over the
+// transformed tile equals the conv of the materialised BN+ReLU output
+__device__ __forceinline__ void bnrelu_chunk(char* p, const float* scale, const float* shift, int c0) {
+  float sc[8], sh[8];
+  load_f8(sc, scale + c0);
+  load_f8(sh, shift + c0);
+  bf16x8 v = *reinterpret_cast<bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = __builtin_fmaf((float)v[j], sc[j], sh[j]);
+    t = t > 0.f ? t : 0.f;
+    v[j] = (__bf16)t;
+  }
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool ADD = false, bool INBN = false>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, NT = 64 * NW;
@@ -1717,6 +1737,21 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     for (int i = wave; i < nxi; i += NW) issue_x_piece(n, p0, i, Xs);
   };
   constexpr int XPW = (HALO_XBUF / 1024 + NW - 1) / NW;  // most pieces per wave and tile
+  // INBN: this wave's pieces of `tile` (landed: after its vmcnt(0)) become
+  // relu(bn(y)) in place; halo and out-of-image pixels stay zero.  Every
+  // wave transforms only what it DMA'd, so the next barrier publishes it.
+  auto xform_x = [&](int tile, char* Xs) {
+    const int R0 = tile * a.TR;
+    const int n = R0 / a.H, p0 = R0 - n * a.H;
+    (void)n;
+    for (int i = wave; i < nxi; i += NW) {
+      const int px = i * 8 + (lane >> 3);
+      const int sr = px / Wp, sc = px - sr * Wp;
+      const int pin = p0 - 1 + sr, win = sc - 1;
+      const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
+      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, a.in_scale, a.in_shift, ((lane & 7) ^ (((px >> 1) & 3) << 1)) * 8);
+    }
+  };
   auto issue_w = [&](int jn) {
     for (int i = wave; i < 72; i += NW) {
       const int tw = i >> 3, col = ((i & 7) << 3) + (lane >> 3);
@@ -1865,7 +1900,10 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     const int jn = u / a.tiles, tile = u - jn * a.tiles;
     char* const Xs = smem + B_BYTES + ((u - u0) & 1) * HALO_XBUF;
     char* const Xn = smem + B_BYTES + ((u - u0 + 1) & 1) * HALO_XBUF;
-    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (first) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (INBN) xform_x(tile, Xs);
+    }
     first = false;
     halo_lds_barrier();
     const int un = u + 1;
@@ -1941,6 +1979,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     // the next tile's rows (issued before the MFMAs) and this wave's older
     // stores retire here; nothing younger is in flight
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (INBN) {
+      if (prefetch && !(a.diag & 4)) xform_x(un - jn * a.tiles, Xn);
+    }
 
     // ---- epilogue
     if constexpr (BNPOST) {
@@ -2197,6 +2238,9 @@ struct HaloWgArgs {
   uint32_t x_bytes;
   int N, H, W, TR, tiles;
   int spread;        // the next tile's pieces among the k-steps' MFMAs (SSIP_HWG_SPREAD=0: ahead of them)
+  // INBN: X is y of the BN+ReLU below; relu(fma(y, in_scale, in_shift)) is
+  // formed in LDS (ssip_conv_wgrad_bnrelu_in)
+  const float *in_scale, *in_shift;
 };
 
 constexpr int HWG_XBUF = 48 * 1024;  // 384 input-image rows x 128 B
@@ -2215,6 +2259,7 @@ __device__ __forceinline__ void read_tfrag(Frag<__bf16>& f, const char* base, in
   f.v = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+template <bool INBN = false>
 __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArgs a) {
   typedef __bf16 T;
   constexpr int NW = 8;
@@ -2259,6 +2304,20 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
     const int R0 = tile * a.TR;
     const int n = R0 / a.H, p0 = R0 - n * a.H;
     for (int i = wave; i < npieces; i += NW) issue_piece(n, p0, i, Xs, Ds);
+  };
+  // INBN: this wave's input-image pieces of `tile` (landed) become
+  // relu(bn(y)) in place; padding and out-of-image pixels stay zero
+  auto xform_x = [&](int tile, char* Xs) {
+    const int R0 = tile * a.TR;
+    const int n = R0 / a.H, p0 = R0 - n * a.H;
+    (void)n;
+    for (int i = wave; i < nxp; i += NW) {
+      const int px = i * 8 + (lane >> 3);
+      const int sr = px / Wp, sc = px - sr * Wp;
+      const int pin = p0 - 1 + sr, win = sc - 1;
+      const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
+      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, a.in_scale, a.in_shift, ((lane & 7) ^ mt64_chunk_xor(px)) * 8);
+    }
   };
   // This wave's pieces of every tile -- i = wave + 8 k: k < 6 input image, k >= 6
   // dy -- as tile-independent byte offsets from the tile's first pixel, with
@@ -2332,6 +2391,9 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
 
   if (u0 < u1) issue(u0, smem0, smem0 + HWG_XBUF);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (INBN) {
+    if (u0 < u1) xform_x(u0, smem0);
+  }
   auto run_tile = [&](int u, char* const Xs, char* const Xn) {
     char* const Ds = Xs + HWG_XBUF;
     halo_lds_barrier();
@@ -2365,6 +2427,9 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's rows land before the barrier
+    if constexpr (INBN) {
+      if (nxt) xform_x(u + 1, Xn);
+    }
   };
   for (int u = u0; u < u1; u += 2) {
     run_tile(u, smem0, smem1);
@@ -3344,7 +3409,8 @@ struct HaloBnPost {
 
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
                        void* out, const void* add, float* partial, hipStream_t st, const float* bias = nullptr,
-                       int relu = 0, const HaloBnPost* bp = nullptr) {
+                       int relu = 0, const HaloBnPost* bp = nullptr, const float* in_scale = nullptr,
+                       const float* in_shift = nullptr) {
   HaloArgs h;
   memset(&h, 0, sizeof(h));
   if (bp) {
@@ -3370,7 +3436,11 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   // 8 waves of 64x32 (16 waves of 32x32 were ~10 % faster in isolation but 3 %
   // slower in the step, where the side streams' kernels run beside them; 4
   // waves of 64x64 slower still: r3-variants branch)
-  if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
+  h.in_scale = in_scale;
+  h.in_shift = in_shift;
+  if (in_scale != nullptr)  // FWD over relu(bn(y)) of the layer below, formed in LDS
+    SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, false, true>), dim3(hp.G), dim3(512), 0, st, h);
+  else if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
     SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bp != nullptr)
     SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 2>), dim3(hp.G), dim3(512), 0, st, h);
@@ -3383,6 +3453,43 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   else
     SSIP_KLAUNCH((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
   return ::ssip::check_launch("conv_halo");
+}
+
+// layer-1 WGRAD on conv_halo_wgrad_kernel + its slab reduce (in_scale: the
+// input is y of the BN+ReLU below, transformed in LDS)
+static int launch_halo_wgrad(const ssip_conv_desc* d, HaloPlan hp, const void* dy, const void* x, float* dw_kcrs,
+                             int c_real, int s_real, int accumulate, void* workspace, int64_t workspace_bytes,
+                             int max_workgroups, hipStream_t st, const float* in_scale, const float* in_shift) {
+  if (max_workgroups > 0) hp.G = std::min(hp.G, max_workgroups);  // persistent: fewer CUs, more tiles each
+  const int64_t hneed = (int64_t)hp.G * 64 * 576 * 4;
+  SSIP_REQUIRE(workspace_bytes >= hneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
+               (long long)workspace_bytes, (long long)hneed);
+  HaloWgArgs h;
+  h.X = static_cast<const __bf16*>(x);
+  h.DY = static_cast<const __bf16*>(dy);
+  h.slab = static_cast<float*>(workspace);
+  h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 64 * 2);
+  h.N = d->N; h.H = d->H; h.W = d->W; h.TR = hp.TR; h.tiles = hp.tiles;
+  static const int spread = [] {
+    const char* e = getenv("SSIP_HWG_SPREAD");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  h.spread = spread;
+  h.in_scale = in_scale;
+  h.in_shift = in_shift;
+  if (in_scale != nullptr)
+    SSIP_KLAUNCH(conv_halo_wgrad_kernel<true>, dim3(hp.G), dim3(512), 0, st, h);
+  else
+    SSIP_KLAUNCH(conv_halo_wgrad_kernel<false>, dim3(hp.G), dim3(512), 0, st, h);
+  int rc = ::ssip::check_launch("conv_halo_wgrad");
+  if (rc) return rc;
+  const long total4 = 64L * 576 / 4;
+  int lg = 0;
+  while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
+  const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
+  SSIP_KLAUNCH(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace, hp.G, 64, 576,
+               c_real, 3, s_real, 64, 3, dw_kcrs, accumulate, lg);
+  return ::ssip::check_launch("wgrad_reduce");
 }
 
 }  // namespace
@@ -3673,34 +3780,9 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
                          hp.G, 64, 224, c_real, d->R, s_real, d->C, d->S, dw_kcrs, accumulate, lg);
       return ::ssip::check_launch("wgrad_reduce");
     }
-    if (halo_wg_plan(d, dtype, hp)) {
-      if (max_workgroups > 0) hp.G = std::min(hp.G, max_workgroups);  // persistent: fewer CUs, more tiles each
-      const int64_t hneed = (int64_t)hp.G * 64 * 576 * 4;
-      SSIP_REQUIRE(workspace_bytes >= hneed, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
-                   (long long)workspace_bytes, (long long)hneed);
-      HaloWgArgs h;
-      h.X = static_cast<const __bf16*>(x);
-      h.DY = static_cast<const __bf16*>(dy);
-      h.slab = static_cast<float*>(workspace);
-      h.x_bytes = (uint32_t)((long)d->N * d->H * d->W * 64 * 2);
-      h.N = d->N; h.H = d->H; h.W = d->W; h.TR = hp.TR; h.tiles = hp.tiles;
-      static const int spread = [] {
-        const char* e = getenv("SSIP_HWG_SPREAD");
-        return (e != nullptr && e[0] == '0') ? 0 : 1;
-      }();
-      h.spread = spread;
-      hipStream_t st = (hipStream_t)stream;
-      SSIP_KLAUNCH(conv_halo_wgrad_kernel, dim3(hp.G), dim3(512), 0, st, h);
-      rc = ::ssip::check_launch("conv_halo_wgrad");
-      if (rc) return rc;
-      const long total4 = 64L * 576 / 4;
-      int lg = 0;
-      while (lg < 6 && (2 << lg) <= hp.G && ((total4 << (lg + 1)) + 255) / 256 <= 1024) ++lg;
-      const long blocks = (total4 + (256 >> lg) - 1) / (256 >> lg);
-      SSIP_KLAUNCH(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float*)workspace,
-                         hp.G, 64, 576, c_real, 3, s_real, 64, 3, dw_kcrs, accumulate, lg);
-      return ::ssip::check_launch("wgrad_reduce");
-    }
+    if (halo_wg_plan(d, dtype, hp))
+      return launch_halo_wgrad(d, hp, dy, x, dw_kcrs, c_real, s_real, accumulate, workspace, workspace_bytes,
+                               max_workgroups, (hipStream_t)stream, nullptr, nullptr);
   }
   pl.args.A = dy; pl.args.B = x; pl.args.out = workspace;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
@@ -3779,6 +3861,33 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
   return ::ssip::check_launch("wgrad_reduce");
 }
 
+
+int ssip_conv_bnrelu_in_supported(const ssip_conv_desc* d, int dtype) {
+  HaloPlan hp, hw;
+  return (halo_plan(MODE_FWD, d, dtype, hp) && halo_wg_plan(d, dtype, hw)) ? 1 : 0;
+}
+
+int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in, const float* in_scale,
+                            const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* stream) {
+  HaloPlan hp;
+  SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype) && halo_plan(MODE_FWD, d, dtype, hp), SSIP_ERR_ARG,
+               "ssip_conv_fwd_bnrelu_in: only the layer-1 halo geometry (3x3 / 1 / 1, 64 -> 64, bf16)");
+  SSIP_REQUIRE(y_in && in_scale && in_shift && w_krsc && y, SSIP_ERR_ARG, "ssip_conv_fwd_bnrelu_in: null pointer");
+  return launch_halo(MODE_FWD, d, hp, y_in, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream, nullptr, 0,
+                     nullptr, in_scale, in_shift);
+}
+
+int ssip_conv_wgrad_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* dy, const void* y_in,
+                              const float* in_scale, const float* in_shift, float* dw_kcrs, int accumulate,
+                              void* workspace, int64_t workspace_bytes, int max_workgroups, void* stream) {
+  HaloPlan hp;
+  SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype) && halo_wg_plan(d, dtype, hp), SSIP_ERR_ARG,
+               "ssip_conv_wgrad_bnrelu_in: only the layer-1 halo geometry (3x3 / 1 / 1, 64 -> 64, bf16)");
+  SSIP_REQUIRE(dy && y_in && in_scale && in_shift && dw_kcrs && workspace && max_workgroups >= 0, SSIP_ERR_ARG,
+               "ssip_conv_wgrad_bnrelu_in: bad arguments");
+  return launch_halo_wgrad(d, hp, dy, y_in, dw_kcrs, d->C, d->S, accumulate, workspace, workspace_bytes,
+                           max_workgroups, (hipStream_t)stream, in_scale, in_shift);
+}
 
 /* Which kernel a conv pass selects for this geometry (tests / tuning): writes a
  * NUL-terminated name such as "glds<fwd,256x256,4x2,2>" or "halo<fwd>" into buf. */

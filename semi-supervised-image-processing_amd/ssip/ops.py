@@ -364,6 +364,45 @@ def conv_wgrad(g: ConvGeom, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
     call(*args)
 
 
+def conv_bnrelu_in_supported(g: ConvGeom, dtype: torch.dtype) -> bool:
+    """The conv can take relu(bn(y)) of the layer below as its input, formed in
+    its LDS tile (the layer-1 halo geometry; ssip_conv_*_bnrelu_in)."""
+    key = ("bri", g, dtype, _plan_env())
+    v = _plan_cache.get(key)
+    if v is None:
+        v = _plan_cache[key] = bool(_lib.lib().ssip_conv_bnrelu_in_supported(g.desc(), _DT[dtype]))
+    return v
+
+
+def conv_fwd_bnrelu_in(g: ConvGeom, y_in: torch.Tensor, in_scale: torch.Tensor, in_shift: torch.Tensor,
+                       w_krsc: torch.Tensor, y: torch.Tensor, partial: Optional[torch.Tensor]) -> None:
+    """conv_fwd(g, relu(y_in * in_scale + in_shift), w_krsc, y, partial) without
+    materialising the BN+ReLU output (bit-identical to bn_apply + conv_fwd)."""
+    assert y_in.numel() == g.N * g.H * g.W * g.C and y.numel() == g.N * g.P * g.Q * g.K
+    assert in_scale.dtype == torch.float32 and in_scale.numel() == g.C and in_shift.numel() == g.C
+    args = ("ssip_conv_fwd_bnrelu_in", g.desc(), dtype_code(y_in), _p(y_in), _p(in_scale), _p(in_shift), _p(w_krsc),
+            _p(y), _p(partial), stream_ptr())
+    if _timer is not None:
+        _timer.wrap("fwd", g.flops(), call, *args, nbytes=_nbytes(y_in, w_krsc, y))
+        return
+    call(*args)
+
+
+def conv_wgrad_bnrelu_in(g: ConvGeom, dy: torch.Tensor, y_in: torch.Tensor, in_scale: torch.Tensor,
+                         in_shift: torch.Tensor, dw: torch.Tensor, accumulate: bool, workspace: torch.Tensor,
+                         max_workgroups: int = 0) -> None:
+    """conv_wgrad with the input relu(y_in * in_scale + in_shift) formed in LDS."""
+    assert dy.numel() == g.N * g.P * g.Q * g.K and y_in.numel() == g.N * g.H * g.W * g.C
+    assert dw.dtype == torch.float32 and dw.numel() == g.K * g.C * g.R * g.S
+    nbytes = workspace.numel() * workspace.element_size()
+    args = ("ssip_conv_wgrad_bnrelu_in", g.desc(), dtype_code(dy), _p(dy), _p(y_in), _p(in_scale), _p(in_shift),
+            _p(dw), int(accumulate), _p(workspace), nbytes, int(max_workgroups), stream_ptr())
+    if _timer is not None:
+        _timer.wrap("wgrad", g.flops(), call, *args, nbytes=_nbytes(dy, y_in, dw) + (dw.numel() * 4 if accumulate else 0))
+        return
+    call(*args)
+
+
 def conv_kernel_name(mode: str, g: ConvGeom, dtype: torch.dtype, max_workgroups: int = 0) -> str:
     """The kernel ssip_conv_{fwd,dgrad,wgrad} selects for g (include/ssip.h);
     max_workgroups: ssip_conv_wgrad_budget's choice under that budget."""

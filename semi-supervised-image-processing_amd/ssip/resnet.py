@@ -167,6 +167,9 @@ class _ConvRec:
     stats: torch.Tensor      # [4, K] mean, invstd, scale, shift
     z: Optional[torch.Tensor] = None   # post BN(+add)+ReLU output (mask source)
     zbits: Optional[torch.Tensor] = None  # its ReLU mask, one bit per element (the backward reads this, not z)
+    # x is y of the BN+ReLU below and this conv forms relu(x * scale + shift)
+    # in its LDS tile (ssip_conv_*_bnrelu_in): (scale, shift)
+    in_bn: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
 
 @dataclass
@@ -405,7 +408,9 @@ def _prepped(model: SSIPResNet, conv: nn.Conv2d, g: ConvGeom, need_t: bool):
 
 
 def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool, save: bool,
-             update_running: bool, in_pad: int = 0) -> _ConvRec:
+             update_running: bool, in_pad: int = 0, in_bn=None) -> _ConvRec:
+    """in_bn = (scale, shift): x is the pre-BN y of the BN+ReLU below, applied
+    inside the conv (train mode, _bnrelu_in_ok geometries)."""
     g = _geom(conv, N, H, W, in_pad)
     dt = model.compute_dtype
     krsc = _prepped(model, conv, g, need_t=save)[0]
@@ -414,7 +419,10 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
     if train:
         nparts = ops.conv_fwd_partial_floats(g)
         partial = torch.empty(nparts, device=x.device, dtype=torch.float32)
-        ops.conv_fwd(g, x, krsc, y, partial)
+        if in_bn is not None:
+            ops.conv_fwd_bnrelu_in(g, x, in_bn[0], in_bn[1], krsc, y, partial)
+        else:
+            ops.conv_fwd(g, x, krsc, y, partial)
         ops.bn_finalize(g.K, ops.conv_fwd_partial_tiles(g, dt), partial, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                         bn.running_var, bn.momentum if bn.momentum is not None else 0.1, bn.eps,
                         update_running, stats[0], stats[1], stats[2], stats[3])
@@ -422,7 +430,17 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
         ops.conv_fwd(g, x, krsc, y, None)
         ops.bn_eval_coeffs(g.K, bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var, bn.eps,
                            stats[0], stats[1], stats[2], stats[3])
-    return _ConvRec(geom=g, conv=conv, bn=bn, x=x, y=y, stats=stats)
+    return _ConvRec(geom=g, conv=conv, bn=bn, x=x, y=y, stats=stats, in_bn=in_bn)
+
+
+# BN+ReLU of a block's first conv applied inside its second conv (layer 1's
+# halo geometry: ssip_conv_fwd_bnrelu_in / ssip_conv_wgrad_bnrelu_in) instead
+# of a separate apply pass (SSIP_BNRELU_IN=0: the apply pass)
+_BNRELU_IN = os.environ.get("SSIP_BNRELU_IN", "1") != "0"
+
+
+def _bnrelu_in_ok(conv, N: int, H: int, W: int, dtype) -> bool:
+    return _BNRELU_IN and ops.conv_bnrelu_in_supported(_geom(conv, N, H, W), dtype)
 
 
 def _conv_bn_ds(model: SSIPResNet, conv, bn, ds_conv, ds_bn, x: torch.Tensor, N, H, W, train: bool, save: bool,
@@ -525,18 +543,26 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
         stages = blk.stages()
         ds = None
         fuse_ds = _fwd_ds_fusable(blk, N, Hc, Wc)
+        in_bn = None
         for i, (conv, bn) in enumerate(stages):
             if i == 0 and fuse_ds:
                 r, ds = _conv_bn_ds(model, conv, bn, blk.downsample[0], blk.downsample[1], z, N, h, w, train, save,
                                     upd)
             else:
-                r = _conv_bn(model, conv, bn, z, N, h, w, train, save, upd)
+                r = _conv_bn(model, conv, bn, z, N, h, w, train, save, upd, in_bn=in_bn)
+            in_bn = None
             h, w = r.geom.P, r.geom.Q
             if i < len(stages) - 1:
-                zz = torch.empty_like(r.y)
-                ops.bn_apply(N * h * w, r.geom.K, r.y, r.stats[2], r.stats[3], None, True, zz)
-                r.z = zz
-                z = zz
+                if train and _bnrelu_in_ok(stages[i + 1][0], N, h, w, dt):
+                    # the next conv applies this BN+ReLU itself; its input and
+                    # its wgrad's stay the pre-BN y (the backward's mask comes
+                    # from y and the affine, so z is never needed)
+                    z, in_bn = r.y, (r.stats[2], r.stats[3])
+                else:
+                    zz = torch.empty_like(r.y)
+                    ops.bn_apply(N * h * w, r.geom.K, r.y, r.stats[2], r.stats[3], None, True, zz)
+                    r.z = zz
+                    z = zz
             recs.append(r)
         last = recs[-1]
         out = torch.empty_like(last.y)
@@ -861,6 +887,16 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         if not w.requires_grad:
             return
         tgt, acc = _grad_target(w, arena)
+        if rec.in_bn is not None:
+            budget = _side_wgrad_budget(rec.geom, dy.dtype, dev) if (side is not None or WGRAD_BUDGET_SERIAL) else 0
+            if side is not None:
+                ops.wait_stream(side, main)
+            with torch.cuda.stream(side if side is not None else main):
+                ops.conv_wgrad_bnrelu_in(rec.geom, dy, rec.x, rec.in_bn[0], rec.in_bn[1], tgt, acc, workspace,
+                                         max_workgroups=budget)
+            if side is not None:
+                dy.record_stream(side)
+            return
         if side is None:
             ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
                            max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev) if WGRAD_BUDGET_SERIAL else 0)

@@ -288,6 +288,166 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_apply_kernel(
   }
 }
 
+// The ResNet stem's case (bf16, C = 64, 3x3 / 2 / pad 1, even H and W), VALU-
+// lean: the generic kernel above spends ~10 VALU ops per window tap and channel
+// (bf16 -> f32, BN, ReLU, rounding, a float compare and three selects) and
+// recomputes every z 2.25 times (overlapping windows): ~825 ops per 8-channel
+// output, which made it VALU-bound (180 us at batch 256, 3.7 TB/s).  Here
+//  * each thread walks R pooled rows of one (column q, 8-channel chunk),
+//    carrying input row 2p+1 into the next pooled row's window (row 2p-1):
+//    6 new taps per output instead of 9;
+//  * z is formed on channel pairs: one packed fma, one packed bf16 rounding,
+//    then ReLU in the integer domain: a saturating +0x7f and a signed max with
+//    0x7f map every negative value, -0.0 and NaN to 0x7f -- the code of 0 --
+//    and keep every z >= 0 in order (z + 0x7f <= 0x7fff): the same order and
+//    ties as bf16(relu(fma(y, scale, shift))) with the generic kernel's
+//    `t > 0 ? t : 0` (NaN -> 0), i.e. ssip_bn_apply's stored value;
+//  * the window max with torch's first-max tie break is one signed 32-bit
+//    max over keys (z' << 16) | (15 - t): equal z prefer the smaller tap index
+//    t, and a padding tap (all ones) is negative and never wins.  The argmax
+//    and the pre-BN y there follow the winning key.
+// Bit-identical outputs, argmax bytes and ymax to the generic kernel
+// (tests/test_gpu_ops.py).
+namespace stem_pool {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef short s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+
+// z' = z + 0x7f per channel of a pair (0x7f = relu'd zero, NaN or negative)
+__device__ __forceinline__ uint32_t zpair(uint32_t ydw, f2 sc, f2 sh) {
+  f2 yv;
+  yv.x = __builtin_bit_cast(float, ydw << 16);
+  yv.y = __builtin_bit_cast(float, ydw & 0xffff0000u);
+  const f2 t = __builtin_elementwise_fma(yv, sc, sh);
+  const bf2 b = __builtin_convertvector(t, bf2);
+  const u2 a = __builtin_elementwise_add_sat(__builtin_bit_cast(u2, b), (u2){0x7f, 0x7f});
+  const s2 r = __builtin_elementwise_max(__builtin_bit_cast(s2, a), (s2){0x7f, 0x7f});
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+}  // namespace stem_pool
+
+template <bool YMAX>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
+                                                                    const __bf16* __restrict__ y,
+                                                                    const float* __restrict__ scale,
+                                                                    const float* __restrict__ shift,
+                                                                    __bf16* __restrict__ out,
+                                                                    uint8_t* __restrict__ idx,
+                                                                    __bf16* __restrict__ ymax) {
+  using namespace stem_pool;
+  constexpr int C = 64;
+  const int q = threadIdx.x >> 3, cc = threadIdx.x & 7;
+  if (q >= Q) return;
+  const int groups = (P + R - 1) / R;
+  const int n = blockIdx.x / groups, p0 = (blockIdx.x - n * groups) * R;
+  const int p1 = p0 + R < P ? p0 + R : P;
+  f2 sc[4], sh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    sc[i] = *reinterpret_cast<const f2*>(scale + cc * 8 + 2 * i);
+    sh[i] = *reinterpret_cast<const f2*>(shift + cc * 8 + 2 * i);
+  }
+  const char* yb = reinterpret_cast<const char*>(y + (long)n * H * W * C + cc * 8);
+  const bool left = q == 0;  // column 2q - 1 is padding
+  const long c0 = (long)(left ? 0 : 2 * q - 1) * C * 2, c1 = (long)(2 * q) * C * 2, c2 = c1 + C * 2;
+  auto load_row = [&](int h, uint4 (&v)[3]) {
+    const char* rp = yb + (long)h * W * C * 2;
+    v[0] = *reinterpret_cast<const uint4*>(rp + c0);
+    v[1] = *reinterpret_cast<const uint4*>(rp + c1);
+    v[2] = *reinterpret_cast<const uint4*>(rp + c2);
+  };
+  // z' pairs of one input row's three taps (padding column: all ones)
+  auto z_row = [&](const uint4 (&v)[3], uint32_t (&z)[3][4]) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t zz = zpair(d[i], sc[i], sh[i]);
+        z[u][i] = (u == 0 && left) ? 0xffffffffu : zz;
+      }
+    }
+  };
+  int32_t best[8];
+  uint32_t ysel[8];
+  // fold one input row (window row r) into the running keys
+  auto fold = [&](const uint32_t (&z)[3][4], const uint4 (&v)[3], int r) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const uint32_t yd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      const uint32_t lo = 15 - (r * 3 + u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t zd = z[u][j >> 1];
+        const int32_t key = (int32_t)((j & 1) ? ((zd & 0xffff0000u) | lo) : ((zd << 16) | lo));
+        if (YMAX) {
+          const bool gt = key > best[j];
+          best[j] = gt ? key : best[j];
+          ysel[j] = gt ? yd[j >> 1] : ysel[j];
+        } else {
+          best[j] = key > best[j] ? key : best[j];
+        }
+      }
+    }
+  };
+  uint32_t zt[3][4];  // window row 0 (input row 2p - 1)
+  uint4 vt[3];
+  if (p0 == 0) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      vt[u] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) zt[u][i] = 0xffffffffu;
+    }
+  } else {
+    load_row(2 * p0 - 1, vt);
+    z_row(vt, zt);
+  }
+  uint4 a[3], b[3];
+  load_row(2 * p0, a);
+  load_row(2 * p0 + 1, b);
+  for (int p = p0; p < p1; ++p) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = 0; ysel[j] = 0; }
+    fold(zt, vt, 0);
+    uint32_t zm[3][4];
+    z_row(a, zm);
+    fold(zm, a, 1);
+    z_row(b, zt);  // window row 2 now, row 0 of the next pooled row
+#pragma unroll
+    for (int u = 0; u < 3; ++u) vt[u] = b[u];
+    if (p + 1 < p1) {  // the next pooled row's two new input rows, in flight during the selection
+      load_row(2 * p + 2, a);
+      load_row(2 * p + 3, b);
+    }
+    fold(zt, vt, 2);
+    uint4 o, ym;
+    uint32_t od[4], yd[4];
+    uint32_t ilo = 0, ihi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t zz = ((uint32_t)best[2 * i] >> 16) | ((uint32_t)best[2 * i + 1] & 0xffff0000u);
+      od[i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, zz) - (u2){0x7f, 0x7f});
+      yd[i] = (ysel[2 * i] & 0xffffu) | (ysel[2 * i + 1] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t t = 15u - ((uint32_t)best[j] & 15u);
+      if (j < 4) ilo |= t << (8 * j); else ihi |= t << (8 * (j - 4));
+    }
+    o.x = od[0]; o.y = od[1]; o.z = od[2]; o.w = od[3];
+    ym.x = yd[0]; ym.y = yd[1]; ym.z = yd[2]; ym.w = yd[3];
+    const long oi = (((long)n * P + p) * Q + q) * C + cc * 8;
+    *reinterpret_cast<uint4*>(out + oi) = o;
+    *reinterpret_cast<uint2*>(idx + oi) = make_uint2(ilo, ihi);
+    if (YMAX) *reinterpret_cast<uint4*>(ymax + oi) = ym;
+  }
+}
+
 // full-resolution rows (n, h) per reduction workgroup: ~8192 workgroups
 // (each thread's gather chain is serial: parallelism comes from workgroups)
 static int rows_per_block(int N, int H) {
@@ -306,6 +466,20 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
                SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: bad arguments");
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   SSIP_REQUIRE((long)N * H * W * C < (1l << 31), SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: too large");
+  const char* pr = std::getenv("SSIP_POOL_ROWS");  // pooled rows per workgroup of the k3s2 kernel; 0: generic
+  const int pool_rows = pr ? std::atoi(pr) : 4;
+  if (dtype == SSIP_BF16 && C == 64 && k == 3 && s == 2 && pad == 1 && H % 2 == 0 && W % 2 == 0 &&
+      Q * 8 <= 512 && pool_rows > 0) {
+    const int groups = (P + pool_rows - 1) / pool_rows;
+    const dim3 grid(N * groups), block((Q * 8 + 63) / 64 * 64);
+    if (ymax)
+      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<true>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
+                   (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)ymax);
+    else
+      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<false>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
+                   (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)nullptr);
+    return ::ssip::check_launch("stem_bn_pool_fwd");
+  }
   SSIP_DISPATCH_DTYPE(dtype, T, {
     SSIP_KLAUNCH(stem_bn_pool_fwd_kernel<T>, dim3(N * P), dim3(256), 0, (hipStream_t)stream, H, W, C, P, Q,
                        k, s, pad, (const T*)y, scale, shift, (T*)out, idx, (T*)ymax);

@@ -693,6 +693,9 @@ _side_budgets = {}
 _HALO_WG_FRAC = float(os.environ.get("SSIP_HALO_WG_FRAC", "0.5"))  # share of the CUs for the layer-1 wgrad
 
 
+_LAST_WG_FULL = os.environ.get("SSIP_LAST_WG_FULL", "0") == "1"
+
+
 def _side_wgrad_budget(g, dtype, dev: torch.device) -> int:
     """Grid cap of a wgrad on the side stream, beside the main stream's dgrad /
     BN-backward chain (ssip_conv_wgrad_budget): the split-K LDS-DMA wgrads one
@@ -882,13 +885,15 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                         partial, coef_buf[: 6 * g.K], mbits)
         return dya, dyb
 
-    def conv_wgrad(rec: _ConvRec, dy):
+    def conv_wgrad(rec: _ConvRec, dy, last: bool = False):
         w = rec.conv.weight
         if not w.requires_grad:
             return
         tgt, acc = _grad_target(w, arena)
         if rec.in_bn is not None:
             budget = _side_wgrad_budget(rec.geom, dy.dtype, dev) if (side is not None or WGRAD_BUDGET_SERIAL) else 0
+            if last and _LAST_WG_FULL:
+                budget = 0
             if side is not None:
                 ops.wait_stream(side, main)
             with torch.cuda.stream(side if side is not None else main):
@@ -907,7 +912,7 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         ops.wait_stream(side, main)
         with torch.cuda.stream(side):
             ops.conv_wgrad(rec.geom, dy, rec.x, tgt, acc, workspace,
-                           max_workgroups=_side_wgrad_budget(rec.geom, dy.dtype, dev))
+                           max_workgroups=0 if (last and _LAST_WG_FULL) else _side_wgrad_budget(rec.geom, dy.dtype, dev))
         dy.record_stream(side)
 
     def conv_dgrad(rec: _ConvRec, dy, out, add=None):
@@ -965,7 +970,9 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
         dxin = None
         for i in range(len(recs) - 1, -1, -1):
             r = recs[i]
-            conv_wgrad(r, g_cur)
+            # the trunk's last wgrad (the first block's first conv) runs beside
+            # only the stem's BN-backward reduction
+            conv_wgrad(r, g_cur, last=(bi == 0 and i == 0 and ds is None))
             if i > 0:
                 dzp = torch.empty_like(r.x)
                 fused = conv_dgrad_bn(r, g_cur, recs[i - 1], dzp)

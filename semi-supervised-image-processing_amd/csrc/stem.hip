@@ -329,7 +329,10 @@ __device__ __forceinline__ uint32_t zpair(uint32_t ydw, f2 sc, f2 sh) {
 
 }  // namespace stem_pool
 
-template <bool YMAX>
+// YMAX 0: no ymax; 1: ymax follows the winning key (a compare + select per
+// tap); 2: the nine taps' y go to the thread's own LDS slots and ymax is read
+// back at the argmax (no per-tap select)
+template <int YMAX>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
                                                                     const __bf16* __restrict__ y,
@@ -374,6 +377,8 @@ stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
   };
   int32_t best[8];
   uint32_t ysel[8];
+  __shared__ uint4 ylds[YMAX == 2 ? 512 * 9 : 1];
+  uint4* mine = ylds + (YMAX == 2 ? threadIdx.x * 9 : 0);
   // fold one input row (window row r) into the running keys
   auto fold = [&](const uint32_t (&z)[3][4], const uint4 (&v)[3], int r) {
 #pragma unroll
@@ -384,7 +389,7 @@ stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
       for (int j = 0; j < 8; ++j) {
         const uint32_t zd = z[u][j >> 1];
         const int32_t key = (int32_t)((j & 1) ? ((zd & 0xffff0000u) | lo) : ((zd << 16) | lo));
-        if (YMAX) {
+        if (YMAX == 1) {
           const bool gt = key > best[j];
           best[j] = gt ? key : best[j];
           ysel[j] = gt ? yd[j >> 1] : ysel[j];
@@ -413,6 +418,10 @@ stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
   for (int p = p0; p < p1; ++p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { best[j] = 0; ysel[j] = 0; }
+    if (YMAX == 2) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) { mine[u] = vt[u]; mine[3 + u] = a[u]; mine[6 + u] = b[u]; }
+    }
     fold(zt, vt, 0);
     uint32_t zm[3][4];
     z_row(a, zm);
@@ -432,7 +441,16 @@ stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
     for (int i = 0; i < 4; ++i) {
       const uint32_t zz = ((uint32_t)best[2 * i] >> 16) | ((uint32_t)best[2 * i + 1] & 0xffff0000u);
       od[i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, zz) - (u2){0x7f, 0x7f});
-      yd[i] = (ysel[2 * i] & 0xffffu) | (ysel[2 * i + 1] & 0xffff0000u);
+      if (YMAX == 1) yd[i] = (ysel[2 * i] & 0xffffu) | (ysel[2 * i + 1] & 0xffff0000u);
+    }
+    if (YMAX == 2) {
+      const uint16_t* m16 = reinterpret_cast<const uint16_t*>(mine);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t e0 = m16[(15u - ((uint32_t)best[2 * i] & 15u)) * 8 + 2 * i];
+        const uint32_t e1 = m16[(15u - ((uint32_t)best[2 * i + 1] & 15u)) * 8 + 2 * i + 1];
+        yd[i] = e0 | (e1 << 16);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -472,11 +490,15 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
       Q * 8 <= 512 && pool_rows > 0) {
     const int groups = (P + pool_rows - 1) / pool_rows;
     const dim3 grid(N * groups), block((Q * 8 + 63) / 64 * 64);
-    if (ymax)
-      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<true>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
+    const char* lm = std::getenv("SSIP_POOL_LDS");  // ymax from LDS slots (default) or per-tap selects
+    if (ymax && (lm == nullptr || std::atoi(lm) != 0))
+      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<2>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
+                   (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)ymax);
+    else if (ymax)
+      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<1>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
                    (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)ymax);
     else
-      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<false>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
+      SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<0>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
                    (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)nullptr);
     return ::ssip::check_launch("stem_bn_pool_fwd");
   }

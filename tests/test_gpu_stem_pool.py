@@ -22,8 +22,9 @@ SHAPES = [
 ]
 
 
-def _run(monkeypatch, rows, N, H, W, y, scale, shift, with_ymax):
+def _run(monkeypatch, rows, N, H, W, y, scale, shift, with_ymax, lds=0):
     monkeypatch.setenv("SSIP_POOL_ROWS", str(rows))
+    monkeypatch.setenv("SSIP_POOL_LDS", str(lds))
     P, Q = H // 2, W // 2
     dev = y.device
     pool = torch.full((N, P, Q, 64), 3.0, device=dev, dtype=torch.bfloat16)
@@ -62,10 +63,11 @@ def test_k3s2_equals_generic(dev, monkeypatch, shape, special):
     N, H, W = shape
     y, scale, shift = _inputs(N, H, W, dev, 5, special)
     ref = _run(monkeypatch, 0, N, H, W, y, scale, shift, True)
-    for rows in (4, 3, 1):
-        got = _run(monkeypatch, rows, N, H, W, y, scale, shift, True)
-        for a, b in zip(got, ref):
-            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), rows
+    for rows in (4, 3, 1, 8):
+        for lds in (0, 1):
+            got = _run(monkeypatch, rows, N, H, W, y, scale, shift, True, lds)
+            for a, b in zip(got, ref):
+                assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), (rows, lds)
         p2, i2, _ = _run(monkeypatch, rows, N, H, W, y, scale, shift, False)
         assert torch.equal(p2.view(torch.uint8), ref[0].view(torch.uint8))
         assert torch.equal(i2, ref[1])

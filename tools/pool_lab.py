@@ -17,6 +17,7 @@ from tune_conv import time_fn  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", default="0,4,2,8")
+    ap.add_argument("--lds", default="0", help="SSIP_POOL_LDS values (ymax from the thread's LDS slots)")
     ap.add_argument("--iters", type=int, default=30)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -29,11 +30,14 @@ def main():
         idx = torch.empty(N, 56, 56, 64, device=dev, dtype=torch.uint8)
         ymax = torch.empty_like(pool) if with_ymax else None
         nbytes = y.numel() * 2 + pool.numel() * (2 + 1 + (2 if with_ymax else 0))
-        for r in a.rows.split(","):
-            os.environ["SSIP_POOL_ROWS"] = r
-            t = time_fn(lambda: ops.stem_bn_pool_fwd(N, H, W, 64, 3, 2, 1, y, scale, shift, pool, idx, ymax),
-                        a.iters)
-            print(f"N={N:3d} ymax={int(with_ymax)} rows={r:>2s} {t:7.1f} us {nbytes / t / 1e6:5.2f} TB/s", flush=True)
+        for lds in a.lds.split(","):
+            os.environ["SSIP_POOL_LDS"] = lds
+            for r in a.rows.split(","):
+                os.environ["SSIP_POOL_ROWS"] = r
+                t = time_fn(lambda: ops.stem_bn_pool_fwd(N, H, W, 64, 3, 2, 1, y, scale, shift, pool, idx, ymax),
+                            a.iters)
+                print(f"N={N:3d} ymax={int(with_ymax)} lds={lds} rows={r:>2s} {t:7.1f} us "
+                      f"{nbytes / t / 1e6:5.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":

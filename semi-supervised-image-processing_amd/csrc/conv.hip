@@ -1588,7 +1588,9 @@ struct HaloArgs {
   const float *in_scale, *in_shift;
   int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 4 no input-row DMA after the
              // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt);
-             // 16 (results right): the next tile's rows issued before the MFMAs, not among them
+             // 16 (results right): the next tile's rows issued before the MFMAs, not among them;
+             // 32 (results right, INBN): the BN+ReLU transform after the k-loop, not inside it;
+             // 64 (INBN, results wrong): no transform
 };
 
 constexpr int HALO_XBUF = 44 * 1024;
@@ -1682,10 +1684,16 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
 // relu(fma(v, scale, shift)) over the 8 channels c0 .. c0 + 7 of one LDS
 // chunk, in place -- bn_apply_kernel's arithmetic exactly, so a conv over the
 // transformed tile equals the conv of the materialised BN+ReLU output
-__device__ __forceinline__ void bnrelu_chunk(char* p, const float* scale, const float* shift, int c0) {
-  float sc[8], sh[8];
-  load_f8(sc, scale + c0);
-  load_f8(sh, shift + c0);
+__device__ __forceinline__ bf16x8 bnrelu8(bf16x8 v, const float (&sc)[8], const float (&sh)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = __builtin_fmaf((float)v[j], sc[j], sh[j]);
+    t = t > 0.f ? t : 0.f;
+    v[j] = (__bf16)t;
+  }
+  return v;
+}
+__device__ __forceinline__ void bnrelu_chunk(char* p, const float (&sc)[8], const float (&sh)[8]) {
   bf16x8 v = *reinterpret_cast<bf16x8*>(p);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -1740,7 +1748,18 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   // INBN: this wave's pieces of `tile` (landed: after its vmcnt(0)) become
   // relu(bn(y)) in place; halo and out-of-image pixels stay zero.  Every
   // wave transforms only what it DMA'd, so the next barrier publishes it.
+  // A lane's LDS chunk is (lane & 7) ^ xtile swizzle of px = 8 i + lane / 8,
+  // i.e. ((px >> 1) & 3) = (lane >> 4) & 3 for every piece i: the lane's
+  // eight channels, and so its scale / shift, are fixed for the whole kernel
+  // (loaded once here; per piece they were a dependent L2 round trip each)
+  float isc[8], ish[8];
+  if constexpr (INBN) {
+    const int c0 = ((lane & 7) ^ (((lane >> 4) & 3) << 1)) * 8;
+    load_f8(isc, a.in_scale + c0);
+    load_f8(ish, a.in_shift + c0);
+  }
   auto xform_x = [&](int tile, char* Xs) {
+    if (a.diag & 64) return;  // ablation: no transform (results wrong)
     const int R0 = tile * a.TR;
     const int n = R0 / a.H, p0 = R0 - n * a.H;
     (void)n;
@@ -1749,8 +1768,27 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
       const int sr = px / Wp, sc = px - sr * Wp;
       const int pin = p0 - 1 + sr, win = sc - 1;
       const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
-      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, a.in_scale, a.in_shift, ((lane & 7) ^ (((px >> 1) & 3) << 1)) * 8);
+      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, isc, ish);
     }
+  };
+  // INBN register staging of the next tile's pieces (XLAG + 1 slots)
+  constexpr int XLAG = 2;
+  bf16x8 xr[XLAG + 1];
+  bool xok[XLAG + 1];
+  auto xreg_load = [&](int n, int p0, int i, int slot) {
+    const int px = i * 8 + (lane >> 3);
+    const int sr = px / Wp, sc = px - sr * Wp;
+    const int pin = p0 - 1 + sr, win = sc - 1;
+    const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);  // xtile_off's swizzle
+    const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
+    const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
+    xr[slot] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsX, ok ? off : SSIP_OOB, 0, 0));
+    xok[slot] = ok;
+  };
+  auto xreg_store = [&](int i, int slot, char* Xs) {
+    bf16x8 v = xr[slot];
+    if (xok[slot]) v = bnrelu8(v, isc, ish);
+    *reinterpret_cast<bf16x8*>(Xs + i * 1024 + lane * 16) = v;
   };
   auto issue_w = [&](int jn) {
     for (int i = wave; i < 72; i += NW) {
@@ -1972,7 +2010,25 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
         for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
       if (st % 2 == 0 && st / 2 < XPW) {
         const int i = wave + (st / 2) * NW;
-        if (spread && i < nxi) issue_x_piece(nn, np0, i, Xn);
+        if constexpr (INBN) {
+          // INBN: the piece comes through registers -- a buffer load now, the
+          // BN+ReLU and one LDS store XLAG pieces later (by then it has
+          // landed) -- so the transform needs no LDS read-modify-write pass and
+          // its VALU work sits between k-steps beside the partner wave's MFMAs
+          // (issued unconditionally -- an unneeded piece reads the OOB zero --
+          // so the compiler can count the loads in flight: vmcnt(XLAG) before
+          // a store instead of vmcnt(0))
+          xreg_load(nn, np0, i, (st / 2) % (XLAG + 1));
+          if ((a.diag & 32) && spread && i < nxi) issue_x_piece(nn, np0, i, Xn);
+        } else {
+          if (spread && i < nxi) issue_x_piece(nn, np0, i, Xn);
+        }
+      }
+      if constexpr (INBN) {
+        if (st % 2 == 0 && st / 2 >= XLAG && st / 2 - XLAG < XPW) {
+          const int k = st / 2 - XLAG, i = wave + k * NW;
+          if (spread && !(a.diag & 32) && i < nxi) xreg_store(i, k % (XLAG + 1), Xn);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1980,7 +2036,14 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     // stores retire here; nothing younger is in flight
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (INBN) {
-      if (prefetch && !(a.diag & 4)) xform_x(un - jn * a.tiles, Xn);
+      // pieces staged too late for the k-loop's stores (XPW + XLAG > 9)
+#pragma unroll
+      for (int k = 9 - XLAG; k < XPW; ++k) {
+        const int i = wave + k * NW;
+        if (spread && !(a.diag & 32) && k >= 0 && i < nxi) xreg_store(i, k % (XLAG + 1), Xn);
+      }
+      // DMA'd pieces (diag 32, or the non-spread order) are transformed in place
+      if (prefetch && !(a.diag & 4) && ((a.diag & 32) || !spread)) xform_x(un - jn * a.tiles, Xn);
     }
 
     // ---- epilogue
@@ -2307,16 +2370,22 @@ __global__ void __launch_bounds__(512, 2) conv_halo_wgrad_kernel(const HaloWgArg
   };
   // INBN: this wave's input-image pieces of `tile` (landed) become
   // relu(bn(y)) in place; padding and out-of-image pixels stay zero
+  // (a lane's chunk, (lane & 7) ^ mt64_chunk_xor(8 i + lane / 8), depends on i
+  // only through i & 1 = wave & 1: one scale / shift load per call, not per piece)
   auto xform_x = [&](int tile, char* Xs) {
     const int R0 = tile * a.TR;
     const int n = R0 / a.H, p0 = R0 - n * a.H;
     (void)n;
+    float isc[8], ish[8];
+    const int c0 = ((lane & 7) ^ mt64_chunk_xor(wave * 8 + (lane >> 3))) * 8;
+    load_f8(isc, a.in_scale + c0);
+    load_f8(ish, a.in_shift + c0);
     for (int i = wave; i < nxp; i += NW) {
       const int px = i * 8 + (lane >> 3);
       const int sr = px / Wp, sc = px - sr * Wp;
       const int pin = p0 - 1 + sr, win = sc - 1;
       const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
-      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, a.in_scale, a.in_shift, ((lane & 7) ^ mt64_chunk_xor(px)) * 8);
+      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, isc, ish);
     }
   };
   // This wave's pieces of every tile -- i = wave + 8 k: k < 6 input image, k >= 6

@@ -235,6 +235,11 @@ class SSIPResNet(nn.Module):
         # before it reads conv1.weight.grad.
         self.defer_stem_wgrad_join = False
         self._pending_side = None
+        # (single process, SemiStep) called once the backward has enqueued every
+        # gradient of the blocks from `early_update_block` up and of the head:
+        # early_update(stream that holds the last of those wgrads)
+        self.early_update = None
+        self.early_update_block = -1
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -1002,6 +1007,8 @@ def _backward_impl(model: SSIPResNet, sv: _Saved, dlogits: torch.Tensor, main, s
                     conv_dgrad(ds, dy_ds, dxin, dxin)
         if hook is not None:
             hook(list(blocks[bi].parameters()))
+        if model.early_update is not None and bi == model.early_update_block:
+            model.early_update(side if side is not None else main)
         dz = dxin
         if dz is None:
             return

@@ -59,6 +59,15 @@ def _common_base(params):
     return b if o == b.shape[0] else None
 
 
+# SSIP_EARLY_ADAMW=1: AdamW of the head and layers 2-4 on its own stream as
+# soon as their gradients are final (during the layer-1 backward) instead of
+# in the step's tail beside the stem wgrad, where both are HBM-bound (single
+# process only: with a process group the all-reduce of every bucket comes
+# first).  Bit-identical updates; measured 5.879 vs 5.849 ms (4 + 4): the
+# layer-1 backward loses more to it than the tail gains.  Off by default.
+_EARLY_ADAMW = os.environ.get("SSIP_EARLY_ADAMW", "0") == "1"
+
+
 class SemiStep:
     """One call = one optimizer step.
 
@@ -119,6 +128,9 @@ class SemiStep:
         # (scoped to this step's own backward: _fwd_bwd sets the model flag and
         # clears it, so another trainer of the same model never defers)
         self._defer = bucketer is None and not graph and os.environ.get("SSIP_DEFER_STEM") != "0"
+        self._upd = None          # the early AdamW's stream
+        self._early_ids = None
+        self._early_done = False
 
     def _side_stream(self, dev):
         if self._side is None:
@@ -245,10 +257,15 @@ class SemiStep:
             ops.wait_stream(main, side)
             zw.record_stream(main)
         m.defer_stem_wgrad_join = self._defer
+        self._early_done = False
+        if self._early_ok(main, side):
+            m.early_update = self._early_update
+            m.early_update_block = len(m.layer1)
         try:
             return self._loss_bwd(logits, y_l, zw)
         finally:
             m.defer_stem_wgrad_join = False
+            m.early_update = None
 
     def __call__(self, x_l: torch.Tensor, y_l: torch.Tensor, x_u: torch.Tensor, params=None) -> StepStats:
         """x_l [Bl,H,W,3] u8, y_l [Bl] int64, x_u [Bu,H,W,3] u8 — all on the device."""
@@ -287,6 +304,32 @@ class SemiStep:
             o += p.shape[0]
         return tuple(out)
 
+    def _early_ok(self, main, side) -> bool:
+        m = self.model
+        return (_EARLY_ADAMW and self.bucketer is None and getattr(self.opt, "dp_bucketer", None) is None
+                and side is not main and self._defer and hasattr(m, "layer1")
+                and len(list(m.blocks())) > len(m.layer1))
+
+    def _early_params(self):
+        """ids of the head's and of layers 2-4's parameters (cached)."""
+        if self._early_ids is None:
+            m = self.model
+            blocks = list(m.blocks())
+            ps = [p for b in blocks[len(m.layer1):] for p in b.parameters()] + list(m.fc.parameters())
+            self._early_ids = {id(p) for p in ps}
+        return self._early_ids
+
+    def _early_update(self, stream) -> None:
+        """AdamW of _early_params on the update stream, after `stream` (which
+        already waited for the main stream's BN gradients of those layers)."""
+        dev = stream.device
+        if self._upd is None:
+            self._upd = torch.cuda.Stream(device=dev)
+        ops.wait_stream(self._upd, stream)
+        with torch.cuda.stream(self._upd):
+            self.opt.step(grad_scale=1.0, only=self._early_params(), join_pending=False)
+        self._early_done = True
+
     def _optimizer_step(self, scale: float) -> None:
         """AdamW; with the stem wgrad still running on the side stream
         (defer_stem_wgrad_join) every other parameter is enqueued first, with
@@ -299,6 +342,19 @@ class SemiStep:
         # round 3's SSIP_STEM_MAIN: 6.399 vs 6.395 ms/step over 3 + 3 alternated
         # runs, no gain -- the simpler layout stays)
         pend = m.take_pending_side()
+        early = self._early_done
+        self._early_done = False
+        if early:
+            # the early launch advanced the device schedule: the rest follow it
+            ops.wait_stream(torch.cuda.current_stream(), self._upd)
+            late_or_early = late | self._early_params()
+            if pend is None:
+                self.opt.step(grad_scale=scale, skip=self._early_params(), sched_step=False)
+                return
+            self.opt.step(grad_scale=scale, skip=late_or_early, join_pending=False, sched_step=False)
+            ops.wait_stream(torch.cuda.current_stream(), pend)
+            self.opt.step(grad_scale=scale, only=late, sched_step=False)
+            return
         if pend is None:
             self.opt.step(grad_scale=scale)
             return
@@ -400,7 +456,10 @@ class SemiStep:
         if self.bucketer is not None:
             self.bucketer.capture_mode = True
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture: with a process group, RCCL's watchdog thread
+        # queries its collectives' events while this thread captures (global
+        # mode turns that into a fatal capture error in the watchdog)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._g_out = self._fwd_bwd(*self._static)
             if self.bucketer is not None:
                 self.bucketer.end_capture()

@@ -330,3 +330,35 @@ def test_plan_step_shape_change_runs_eagerly(dev):
         assert torch.isfinite(out.loss).all()
     assert step._plan is not None and step._static[0].shape[0] == B
     assert step.opt.device_step_count() == 5
+
+
+@pytest.mark.parametrize("plan", [False, True])
+def test_early_adamw_matches_one_update(dev, monkeypatch, plan):
+    """The head's and layers 2-4's AdamW launched on its own stream during the
+    layer-1 backward (semi_step._EARLY_ADAMW) gives the same losses, weights,
+    AdamW moments and device step count, bit for bit, as the updates all
+    launched after the backward: the same elementwise update, only regrouped."""
+    from ssip import semi_step as ss
+    S, Bl, Bu = 64, 8, 8
+    g = torch.Generator().manual_seed(6)
+    x_l = torch.randint(0, 256, (Bl, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    x_u = torch.randint(0, 256, (Bu, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    y_l = torch.randint(0, 2, (Bl,), generator=g).to(dev)
+    runs = []
+    for early in (False, True):
+        monkeypatch.setattr(ss, "_EARLY_ADAMW", early)
+        torch.manual_seed(0)
+        m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2).to(dev).train()
+        step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=S, seed=13, plan=plan)
+        step.opt.use_device_schedule()
+        losses = [step(x_l, y_l, x_u).loss.clone() for _ in range(5)]
+        torch.cuda.synchronize()
+        assert (step._upd is not None) == early
+        runs.append((torch.stack(losses).cpu(), step.arena.flat.detach().cpu().clone(),
+                     [t.detach().cpu().clone() for t in step.opt._flat_state], step.opt.device_step_count()))
+    (l0, w0, s0, t0), (l1, w1, s1, t1) = runs
+    assert t0 == t1 == 5
+    assert torch.equal(l0, l1)
+    assert torch.equal(w0, w1)
+    for a, b in zip(s0, s1):
+        assert torch.equal(a, b)

@@ -343,7 +343,8 @@ stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
                                                                     __bf16* __restrict__ ymax) {
   using namespace stem_pool;
   constexpr int C = 64;
-  const int q = threadIdx.x >> 3, cc = threadIdx.x & 7;
+  // blockIdx.y: a group of 64 pooled columns (one workgroup row covers Q <= 64)
+  const int q = (int)blockIdx.y * 64 + (threadIdx.x >> 3), cc = threadIdx.x & 7;
   if (q >= Q) return;
   const int groups = (P + R - 1) / R;
   const int n = blockIdx.x / groups, p0 = (blockIdx.x - n * groups) * R;
@@ -487,9 +488,9 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
   const char* pr = std::getenv("SSIP_POOL_ROWS");  // pooled rows per workgroup of the k3s2 kernel; 0: generic
   const int pool_rows = pr ? std::atoi(pr) : 4;
   if (dtype == SSIP_BF16 && C == 64 && k == 3 && s == 2 && pad == 1 && H % 2 == 0 && W % 2 == 0 &&
-      Q * 8 <= 512 && pool_rows > 0) {
+      pool_rows > 0) {
     const int groups = (P + pool_rows - 1) / pool_rows;
-    const dim3 grid(N * groups), block((Q * 8 + 63) / 64 * 64);
+    const dim3 grid(N * groups, (Q + 63) / 64), block(Q >= 64 ? 512 : (Q * 8 + 63) / 64 * 64);
     const char* lm = std::getenv("SSIP_POOL_LDS");  // ymax from LDS slots (default) or per-tap selects
     if (ymax && (lm == nullptr || std::atoi(lm) != 0))
       SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<2>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,

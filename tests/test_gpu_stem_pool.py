@@ -18,6 +18,7 @@ SHAPES = [
     (2, 112, 112),  # the stem at 224^2
     (3, 18, 22),    # 9 pooled rows: a remainder for every rows-per-workgroup value
     (1, 8, 128),    # 64 pooled columns: 512 threads
+    (1, 6, 260),    # 130 pooled columns: three column groups, the last partial
     (2, 2, 2),      # one pooled pixel, every window clipped
 ]
 

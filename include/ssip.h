@@ -248,6 +248,8 @@ int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zm
  * ymax (nullable, pooled shape): the forward stores each window's pre-BN
  * argmax value there, and the backward then reduces over the pooled grid
  * (dpool + ymax) instead of gathering the full-resolution map twice.
+ * idx may be NULL when no backward follows (a no-grad forward): the argmax
+ * bytes are then not written.
  * ---------------------------------------------------------------------- */
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
                           const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream);

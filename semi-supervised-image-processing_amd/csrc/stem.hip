@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
       }
       const long oi = ((long)row * Q + q) * C + cc * 8;
       o.store(out + oi);
-      *reinterpret_cast<uint64_t*>(idx + oi) = packed;
+      if (idx) *reinterpret_cast<uint64_t*>(idx + oi) = packed;
       if (ymax) ym.store(ymax + oi);
     }
     return;
@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) stem_bn_pool_fwd_kernel(int H, int W, int
     }
     const long oi = ((long)row * Q + q) * C + cc * 8;
     o.store(out + oi);
-    *reinterpret_cast<uint64_t*>(idx + oi) = packed;
+    if (idx) *reinterpret_cast<uint64_t*>(idx + oi) = packed;
     if (ymax) ym.store(ymax + oi);
   }
 }
@@ -462,7 +462,7 @@ stem_bn_pool_fwd_k3s2_kernel(int H, int W, int P, int Q, int R,
     ym.x = yd[0]; ym.y = yd[1]; ym.z = yd[2]; ym.w = yd[3];
     const long oi = (((long)n * P + p) * Q + q) * C + cc * 8;
     *reinterpret_cast<uint4*>(out + oi) = o;
-    *reinterpret_cast<uint2*>(idx + oi) = make_uint2(ilo, ihi);
+    if (YMAX || idx) *reinterpret_cast<uint2*>(idx + oi) = make_uint2(ilo, ihi);
     if (YMAX) *reinterpret_cast<uint4*>(ymax + oi) = ym;
   }
 }
@@ -481,7 +481,7 @@ extern "C" {
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
                           const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream) {
   SSIP_REQUIRE(N > 0 && H > 0 && W > 0 && C % 8 == 0 && 256 % (C / 8) == 0 && k > 0 && k * k <= 255 && s > 0 &&
-                   y && scale && shift && out && idx,
+                   y && scale && shift && out && (idx || !ymax),
                SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: bad arguments");
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   SSIP_REQUIRE((long)N * H * W * C < (1l << 31), SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: too large");

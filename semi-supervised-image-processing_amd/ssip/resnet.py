@@ -506,7 +506,8 @@ def _forward(model: SSIPResNet, images: torch.Tensor, train: bool, save: bool, i
     Hp = (g.P + 2 * pd - k) // s + 1
     Wp = (g.Q + 2 * pd - k) // s + 1
     pool = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=dt)
-    idx = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=torch.uint8)
+    # (argmax bytes only for a backward: the weak forward writes none)
+    idx = torch.empty((N, Hp, Wp, g.K), device=dev, dtype=torch.uint8) if save else None
     # BN -> ReLU -> max-pool in one pass over y (the full-resolution z is never
     # stored).  (Round 5 measured the window selection inside the stem conv --
     # conv rows 2p-1..2p+1 per pooled row, BN + ReLU after on the pooled grid,

@@ -72,6 +72,12 @@ def test_k3s2_equals_generic(dev, monkeypatch, shape, special):
         p2, i2, _ = _run(monkeypatch, rows, N, H, W, y, scale, shift, False)
         assert torch.equal(p2.view(torch.uint8), ref[0].view(torch.uint8))
         assert torch.equal(i2, ref[1])
+        # a no-grad forward: no argmax bytes, the same pooled values
+        monkeypatch.setenv("SSIP_POOL_ROWS", str(rows))
+        p3 = torch.full_like(ref[0], 3.0)
+        ops.stem_bn_pool_fwd(N, H, W, 64, 3, 2, 1, y, scale, shift, p3, None, None)
+        torch.cuda.synchronize()
+        assert torch.equal(p3.view(torch.uint8), ref[0].view(torch.uint8))
 
 
 @pytest.mark.parametrize("special", [False, True])

@@ -156,10 +156,15 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
  * Bottleneck (model(inputs) at src/training/common.py:380) where conv2 is the
  * layer-1 3x3 / stride 1 / pad 1, 64 -> 64 conv (the halo kernels); the
  * weight gradient of the same conv takes the same input.  Bit-identical to
- * ssip_bn_apply followed by ssip_conv_fwd / ssip_conv_wgrad. */
+ * ssip_bn_apply followed by ssip_conv_fwd / ssip_conv_wgrad.  z_out
+ * (nullable, [N][H][W][C]): the forward also writes the transformed input
+ * there (= ssip_bn_apply's output, each row once) for a later plain
+ * ssip_conv_wgrad, which is cheaper than ssip_conv_wgrad_bnrelu_in beside
+ * another stream. */
 int ssip_conv_bnrelu_in_supported(const ssip_conv_desc* d, int dtype);
 int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in, const float* in_scale,
-                            const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* stream);
+                            const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* z_out,
+                            void* stream);
 int ssip_conv_wgrad_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* dy, const void* y_in,
                               const float* in_scale, const float* in_shift, float* dw_kcrs, int accumulate,
                               void* workspace, int64_t workspace_bytes, int max_workgroups, void* stream);

@@ -1586,6 +1586,7 @@ struct HaloArgs {
   // INBN (FWD): the input is y of the BN+ReLU below; x = relu(fma(y, in_scale,
   // in_shift)) is formed in LDS (ssip_conv_fwd_bnrelu_in)
   const float *in_scale, *in_shift;
+  __bf16* zout;  // INBN (nullable): the transformed input's own tile rows written out (the wgrad's x)
   int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 4 no input-row DMA after the
              // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt);
              // 16 (results right): the next tile's rows issued before the MFMAs, not among them;
@@ -1723,6 +1724,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
   const int u0 = (int)((long)g * a.units / G), u1 = (int)((long)(g + 1) * a.units / G);
   const __amdgpu_buffer_rsrc_t rsX = make_rsrc(a.X, a.x_bytes), rsW = make_rsrc(a.Wt, a.w_bytes);
   const __amdgpu_buffer_rsrc_t rsO = make_rsrc(a.out, a.o_bytes), rsA = make_rsrc(a.add, a.o_bytes);
+  const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(a.zout, a.zout ? a.x_bytes : 0);
+  typedef __attribute__((ext_vector_type(4))) unsigned int hv4u;
   const int Wp = a.W + 2;
   const int npx = (a.TR + 2) * Wp;
   const int nxi = (npx + 7) >> 3;  // X DMA wave-instructions per tile (8 pixels each)
@@ -1758,24 +1761,33 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     load_f8(isc, a.in_scale + c0);
     load_f8(ish, a.in_shift + c0);
   }
-  auto xform_x = [&](int tile, char* Xs) {
+  auto xform_x = [&](int tile, char* Xs, bool zst) {
     if (a.diag & 64) return;  // ablation: no transform (results wrong)
     const int R0 = tile * a.TR;
     const int n = R0 / a.H, p0 = R0 - n * a.H;
-    (void)n;
     for (int i = wave; i < nxi; i += NW) {
       const int px = i * 8 + (lane >> 3);
       const int sr = px / Wp, sc = px - sr * Wp;
       const int pin = p0 - 1 + sr, win = sc - 1;
       const bool ok = px < npx && pin >= 0 && pin < a.H && win >= 0 && win < a.W;
-      if (ok) bnrelu_chunk(Xs + i * 1024 + lane * 16, isc, ish);
+      if (ok) {
+        char* const q = Xs + i * 1024 + lane * 16;
+        bnrelu_chunk(q, isc, ish);
+        if (zst && sr >= 1 && sr <= a.TR) {
+          const int ch = (lane & 7) ^ (((px >> 1) & 3) << 1);
+          const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hv4u, *reinterpret_cast<const bf16x8*>(q)),
+                                                 rsZ, off, 0, 0);
+        }
+      }
     }
   };
   // INBN register staging of the next tile's pieces (XLAG + 1 slots)
   constexpr int XLAG = 2;
   bf16x8 xr[XLAG + 1];
   bool xok[XLAG + 1];
-  auto xreg_load = [&](int n, int p0, int i, int slot) {
+  uint32_t xzo[XLAG + 1];  // z_out offset of the piece (SSIP_OOB: halo row, padding or no z_out)
+  auto xreg_load = [&](int n, int p0, int i, int slot, bool zst_tile) {
     const int px = i * 8 + (lane >> 3);
     const int sr = px / Wp, sc = px - sr * Wp;
     const int pin = p0 - 1 + sr, win = sc - 1;
@@ -1784,11 +1796,13 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     const uint32_t off = (uint32_t)(((((long)n * a.H + pin) * a.W + win) * 64 + ch * 8) * 2);
     xr[slot] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsX, ok ? off : SSIP_OOB, 0, 0));
     xok[slot] = ok;
+    xzo[slot] = (ok && zst_tile && sr >= 1 && sr <= a.TR) ? off : SSIP_OOB;
   };
   auto xreg_store = [&](int i, int slot, char* Xs) {
     bf16x8 v = xr[slot];
     if (xok[slot]) v = bnrelu8(v, isc, ish);
     *reinterpret_cast<bf16x8*>(Xs + i * 1024 + lane * 16) = v;
+    if (a.zout) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hv4u, v), rsZ, xzo[slot], 0, 0);
   };
   auto issue_w = [&](int jn) {
     for (int i = wave; i < 72; i += NW) {
@@ -1940,7 +1954,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     char* const Xn = smem + B_BYTES + ((u - u0 + 1) & 1) * HALO_XBUF;
     if (first) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if constexpr (INBN) xform_x(tile, Xs);
+      if constexpr (INBN) xform_x(tile, Xs, a.zout != nullptr && jn == 0);
     }
     first = false;
     halo_lds_barrier();
@@ -2018,7 +2032,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
           // (issued unconditionally -- an unneeded piece reads the OOB zero --
           // so the compiler can count the loads in flight: vmcnt(XLAG) before
           // a store instead of vmcnt(0))
-          xreg_load(nn, np0, i, (st / 2) % (XLAG + 1));
+          xreg_load(nn, np0, i, (st / 2) % (XLAG + 1), a.zout != nullptr && jn == 0);
           if ((a.diag & 32) && spread && i < nxi) issue_x_piece(nn, np0, i, Xn);
         } else {
           if (spread && i < nxi) issue_x_piece(nn, np0, i, Xn);
@@ -2043,7 +2057,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
         if (spread && !(a.diag & 32) && k >= 0 && i < nxi) xreg_store(i, k % (XLAG + 1), Xn);
       }
       // DMA'd pieces (diag 32, or the non-spread order) are transformed in place
-      if (prefetch && !(a.diag & 4) && ((a.diag & 32) || !spread)) xform_x(un - jn * a.tiles, Xn);
+      if (prefetch && !(a.diag & 4) && ((a.diag & 32) || !spread))
+        xform_x(un - jn * a.tiles, Xn, a.zout != nullptr && jn == 0);
     }
 
     // ---- epilogue
@@ -3479,7 +3494,7 @@ struct HaloBnPost {
 static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, const void* X, const void* Wt,
                        void* out, const void* add, float* partial, hipStream_t st, const float* bias = nullptr,
                        int relu = 0, const HaloBnPost* bp = nullptr, const float* in_scale = nullptr,
-                       const float* in_shift = nullptr) {
+                       const float* in_shift = nullptr, void* zout = nullptr) {
   HaloArgs h;
   memset(&h, 0, sizeof(h));
   if (bp) {
@@ -3507,6 +3522,7 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
   // waves of 64x64 slower still: r3-variants branch)
   h.in_scale = in_scale;
   h.in_shift = in_shift;
+  h.zout = static_cast<__bf16*>(zout);
   if (in_scale != nullptr)  // FWD over relu(bn(y)) of the layer below, formed in LDS
     SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, false, true>), dim3(hp.G), dim3(512), 0, st, h);
   else if (bp != nullptr && add == nullptr && bp->bits == nullptr)  // DGRAD + BN-backward reduction
@@ -3937,13 +3953,14 @@ int ssip_conv_bnrelu_in_supported(const ssip_conv_desc* d, int dtype) {
 }
 
 int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in, const float* in_scale,
-                            const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* stream) {
+                            const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* z_out,
+                            void* stream) {
   HaloPlan hp;
   SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype) && halo_plan(MODE_FWD, d, dtype, hp), SSIP_ERR_ARG,
                "ssip_conv_fwd_bnrelu_in: only the layer-1 halo geometry (3x3 / 1 / 1, 64 -> 64, bf16)");
   SSIP_REQUIRE(y_in && in_scale && in_shift && w_krsc && y, SSIP_ERR_ARG, "ssip_conv_fwd_bnrelu_in: null pointer");
   return launch_halo(MODE_FWD, d, hp, y_in, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream, nullptr, 0,
-                     nullptr, in_scale, in_shift);
+                     nullptr, in_scale, in_shift, z_out);
 }
 
 int ssip_conv_wgrad_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* dy, const void* y_in,

@@ -96,7 +96,7 @@ _SIGS = {
     "ssip_conv_wgrad": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _vp]),
     "ssip_conv_wgrad_budget": (_c_int, [_PD, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_i64, _c_int, _vp]),
     "ssip_conv_bnrelu_in_supported": (_c_int, [_PD, _c_int]),
-    "ssip_conv_fwd_bnrelu_in": (_c_int, [_PD, _c_int] + [_vp] * 7),
+    "ssip_conv_fwd_bnrelu_in": (_c_int, [_PD, _c_int] + [_vp] * 8),
     "ssip_conv_wgrad_bnrelu_in": (_c_int, [_PD, _c_int] + [_vp] * 5 + [_c_int, _vp, _c_i64, _c_int, _vp]),
     "ssip_stem_bwd_wgrad_supported": (_c_int, [_PD, _c_int]),
     "ssip_conv_kernel_name": (_c_int, [_c_int, _PD, _c_int, ctypes.c_char_p, _c_int]),

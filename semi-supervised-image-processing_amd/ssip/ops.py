@@ -375,13 +375,17 @@ def conv_bnrelu_in_supported(g: ConvGeom, dtype: torch.dtype) -> bool:
 
 
 def conv_fwd_bnrelu_in(g: ConvGeom, y_in: torch.Tensor, in_scale: torch.Tensor, in_shift: torch.Tensor,
-                       w_krsc: torch.Tensor, y: torch.Tensor, partial: Optional[torch.Tensor]) -> None:
+                       w_krsc: torch.Tensor, y: torch.Tensor, partial: Optional[torch.Tensor],
+                       z_out: Optional[torch.Tensor] = None) -> None:
     """conv_fwd(g, relu(y_in * in_scale + in_shift), w_krsc, y, partial) without
-    materialising the BN+ReLU output (bit-identical to bn_apply + conv_fwd)."""
+    a separate BN+ReLU pass (bit-identical to bn_apply + conv_fwd); z_out
+    (optional, y_in's shape) receives the BN+ReLU output itself, written by the
+    conv as it forms its tiles."""
     assert y_in.numel() == g.N * g.H * g.W * g.C and y.numel() == g.N * g.P * g.Q * g.K
     assert in_scale.dtype == torch.float32 and in_scale.numel() == g.C and in_shift.numel() == g.C
+    assert z_out is None or (z_out.numel() == y_in.numel() and z_out.dtype == y_in.dtype)
     args = ("ssip_conv_fwd_bnrelu_in", g.desc(), dtype_code(y_in), _p(y_in), _p(in_scale), _p(in_shift), _p(w_krsc),
-            _p(y), _p(partial), stream_ptr())
+            _p(y), _p(partial), _p(z_out), stream_ptr())
     if _timer is not None:
         _timer.wrap("fwd", g.flops(), call, *args, nbytes=_nbytes(y_in, w_krsc, y))
         return

@@ -425,7 +425,12 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
         nparts = ops.conv_fwd_partial_floats(g)
         partial = torch.empty(nparts, device=x.device, dtype=torch.float32)
         if in_bn is not None:
-            ops.conv_fwd_bnrelu_in(g, x, in_bn[0], in_bn[1], krsc, y, partial)
+            z = torch.empty_like(x) if (save and _BNRELU_Z) else None
+            ops.conv_fwd_bnrelu_in(g, x, in_bn[0], in_bn[1], krsc, y, partial, z_out=z)
+            if z is not None:
+                # the conv wrote relu(bn(x)) as it formed its tiles: the weight
+                # gradient takes it as a plain input
+                x, in_bn = z, None
         else:
             ops.conv_fwd(g, x, krsc, y, partial)
         ops.bn_finalize(g.K, ops.conv_fwd_partial_tiles(g, dt), partial, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
@@ -442,6 +447,12 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
 # halo geometry: ssip_conv_fwd_bnrelu_in / ssip_conv_wgrad_bnrelu_in) instead
 # of a separate apply pass (SSIP_BNRELU_IN=0: the apply pass)
 _BNRELU_IN = os.environ.get("SSIP_BNRELU_IN", "1") != "0"
+# SSIP_BNRELU_Z=1: with a backward to follow, the conv also writes the BN+ReLU
+# output (each row once, from the tiles it forms) so its weight gradient is the
+# plain halo wgrad (the in-tile transform makes that one 50-100 us longer
+# beside the main stream's layer-1 backward).  Measured 6.216 vs 6.196 ms
+# (4 + 4): the forward's extra 103 MB of stores cost more.  Off by default.
+_BNRELU_Z = os.environ.get("SSIP_BNRELU_Z", "0") == "1"
 
 
 def _bnrelu_in_ok(conv, N: int, H: int, W: int, dtype) -> bool:

@@ -53,6 +53,16 @@ def test_fwd_bnrelu_in_equals_apply_then_conv(dev, shape):
     assert torch.equal(out_y.view(torch.int16), ref_y.view(torch.int16))
     n = ops.conv_fwd_partial_tiles(g, torch.bfloat16) * 64 * 3
     assert torch.equal(out_p[:n], ref_p[:n])
+    # z_out: the BN+ReLU output written by the conv, = bn_apply's, bit for bit;
+    # the conv's own outputs unchanged
+    z = torch.full_like(x, 9.0)
+    out2 = torch.full_like(ref_y, 7.0)
+    out_p2 = torch.zeros(nparts, device=dev)
+    ops.conv_fwd_bnrelu_in(g, y_in, scale, shift, w, out2, out_p2, z_out=z)
+    torch.cuda.synchronize()
+    assert torch.equal(z.view(torch.int16), x.view(torch.int16))
+    assert torch.equal(out2.view(torch.int16), ref_y.view(torch.int16))
+    assert torch.equal(out_p2[:n], ref_p[:n])
     # the input tensor itself is not modified
     x2 = torch.empty_like(x)
     ops.bn_apply(N * H * W, 64, y_in, scale, shift, None, True, x2)

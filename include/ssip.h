@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SSIP_ABI_VERSION 13
+#define SSIP_ABI_VERSION 14
 
 enum ssip_dtype { SSIP_F32 = 0, SSIP_BF16 = 1 };
 enum ssip_status { SSIP_OK = 0, SSIP_ERR_ARG = -1, SSIP_ERR_LAUNCH = -2, SSIP_ERR_WORKSPACE = -3 };
@@ -133,11 +133,12 @@ int ssip_conv_wgrad(const ssip_conv_desc* d, int dtype, const void* dy, const vo
 /* The same with a workgroup budget for the split-K grid of the LDS-DMA wgrad
  * (ABI 10), for a wgrad that shares the chip with another stream's kernels
  * (the backward's side stream beside the dgrad / BN-backward chain); 0 =
- * ssip_conv_wgrad's full-chip grid.  ABI 12: with a budget the bf16 wgrad
- * takes 16-wave 256x256 (K % 256 == 0) or 128x256 tiles that fit one
- * workgroup per CU, and at most max_workgroups of them (split count =
- * floor(max_workgroups / output tiles)); other tiles keep ceil(max_workgroups
- * / tiles) splits ($SSIP_WGRAD_BIG=0: the full-grid tiles).  The persistent
+ * ssip_conv_wgrad's full-chip grid.  By default a budget keeps the full-grid
+ * tiles and sets their split count to ceil(max_workgroups / output tiles).
+ * Only with $SSIP_WGRAD_BIG=1 (or 2: the K % 256 == 0 shapes only) does the
+ * bf16 wgrad take 16-wave 256x256 / 128x256 tiles that fit one workgroup per
+ * CU, at most max_workgroups of them (split count = floor(max_workgroups /
+ * output tiles)); they measured faster alone but slower in the step.  The persistent
  * layer-1 and stem wgrads (one workgroup per CU, all of its LDS) run on at
  * most max_workgroups CUs.  Same result up to the fp32 order of the split /
  * slab sum (fixed for a budget).  The workspace a budget needs:
@@ -258,6 +259,13 @@ int ssip_bn_bwd_dual(int dtype, int64_t M, int C, const void* dz, const void* zm
  * ---------------------------------------------------------------------- */
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
                           const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream);
+/* ABI 14: the kernel ssip_stem_bn_pool_fwd launches for that shape (has_ymax:
+ * a ymax output is passed), as a NUL-terminated name into buf:
+ * "stem_bn_pool_fwd_k3s2<2|1|0>" (bf16, C = 64, 3x3 / stride 2 / pad 1, even
+ * H and W; 2 = ymax from LDS, 1 = per-tap ymax, 0 = no ymax) or
+ * "stem_bn_pool_fwd<generic>".  For tests and profiles; no launch. */
+int ssip_stem_bn_pool_kernel_name(int dtype, int N, int H, int W, int C, int k, int s, int pad, int has_ymax,
+                                  char* buf, int buflen);
 int64_t ssip_stem_pool_bn_bwd_partial_floats(int N, int H, int W, int C);
 /* The stem backward tail fused (bf16, 224x224 input): dW (+)= wgrad of the
  * stem conv with dy = BN-backward apply of the ReLU-masked, argmax-gathered

@@ -107,6 +107,7 @@ struct ConvArgs {
   int ds_from;
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
   int dma_mid;  // LDS-DMA ring: the next stage's pieces after the k-step's reads, before its second MFMA half (SSIP_DMA_MID)
+  int stagger;  // LDS-DMA ring: waves NW/2.. run each k-step's second MFMA half after the next barrier (SSIP_STAGGER)
   // FWD of a 3x3 / stride-s conv fused with its block's 1x1 / stride-s
   // downsample (ssip_conv_fwd_ds): workgroups >= fwd_tiles1 compute the
   // downsample's tiles -- its input pixel is the conv's tap (1, 1) pixel, so
@@ -1306,8 +1307,25 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
   Frag<T> fa[2][FM], fb[2][FN];
+  // Stagger (MI355X_MICROARCH "two waves per SIMD" item 9): waves w and
+  // w + NW/2 share a SIMD and run this loop in lockstep -- both issue their
+  // LDS-DMA pieces and fragment reads right after the barrier with the SIMD's
+  // matrix pipe idle, then both multiply (round 3's ablation: the DMA and MFMA
+  // phases add).  The second half of the workgroup runs each k-step's second
+  // MFMA half after the next barrier instead, from fragments it already holds
+  // in registers, so its matrix work fills the interval in which its partner
+  // issues the ring refill and reads.  LDS is untouched by the deferred half;
+  // the accumulation order h0(ks), h1(ks), h0(ks+1), ... is unchanged, so the
+  // results are the same bits.
+  const bool lag = a.stagger != 0 && wave >= NW / 2;
   for (int ks = 0; ks < nsteps; ++ks) {
     if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
+    if (lag && ks > 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[1][i], fb[1][j]);
+    }
     const bool refill = ks + NSTAGE - 1 < nsteps;
     if (refill && !a.dma_mid) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
     const char* As = smem + stage * STAGE;
@@ -1349,12 +1367,19 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       // (dma_mid: after every fragment read of the step, so no read follows
       // the DMA into the ring before the next step's barrier)
       if (h == 1 && refill && a.dma_mid) issue(ks + NSTAGE - 1, stage == 0 ? NSTAGE - 1 : stage - 1);
+      if (h == 1 && lag) break;  // deferred past the next barrier
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[h][i], fb[h][j]);
     }
     stage = stage == NSTAGE - 1 ? 0 : stage + 1;
+  }
+  if (lag && nsteps > 0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[1][i], fb[1][j]);
   }
   __syncthreads();
   if constexpr (MODE == MODE_DGRAD && POST)
@@ -3050,6 +3075,17 @@ static int apply_force(int mode, int elem_bytes, Plan& pl) {
   return SSIP_OK;
 }
 
+// SSIP_STAGGER (read per plan, so a lab can flip it in one process): a
+// bit mask over the passes whose LDS-DMA ring kernels run the stagger
+// (conv_glds_kernel: waves NW/2.. one MFMA half behind), 1 fwd, 2 dgrad,
+// 4 wgrad; 0 off.
+static int stagger_for(int mode, const Plan& pl) {
+  if (pl.stages <= 0 || pl.conv1) return 0;
+  const char* e = getenv("SSIP_STAGGER");
+  const int m = e != nullptr ? atoi(e) : 0;
+  return (m >> mode) & 1;
+}
+
 static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl, int wg_budget = 0) {
   SSIP_REQUIRE(desc_ok(d), SSIP_ERR_ARG, "bad conv descriptor");
   pl.mode = mode;
@@ -3168,6 +3204,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
     }();
     a.dma_mid = mid == 1 || (mid == 2 && pl.bm == 256 && pl.bn == 256);
   }
+  a.stagger = stagger_for(mode, pl);
   return SSIP_OK;
 }
 

@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(128) stem_pool_bn_bwd_apply_kernel(
 //    t, and a padding tap (all ones) is negative and never wins.  The argmax
 //    and the pre-BN y there follow the winning key.
 // Bit-identical outputs, argmax bytes and ymax to the generic kernel
-// (tests/test_gpu_ops.py).
+// (tests/test_gpu_stem_pool.py; bench geometry: tests/test_gpu_bench_geometry.py).
 namespace stem_pool {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -478,6 +478,28 @@ static int rows_per_block(int N, int H) {
 
 extern "C" {
 
+// the pooled-forward kernel ssip_stem_bn_pool_fwd takes for a shape: 2 / 1 / 0
+// = stem_bn_pool_fwd_k3s2_kernel<ymax from LDS / per-tap ymax / no ymax>,
+// -1 = the generic stem_bn_pool_fwd_kernel
+static int pool_fwd_variant(int dtype, int H, int W, int C, int k, int s, int pad, bool ymax) {
+  const char* pr = std::getenv("SSIP_POOL_ROWS");  // pooled rows per workgroup of the k3s2 kernel; 0: generic
+  const int pool_rows = pr ? std::atoi(pr) : 4;
+  if (!(dtype == SSIP_BF16 && C == 64 && k == 3 && s == 2 && pad == 1 && H % 2 == 0 && W % 2 == 0 && pool_rows > 0))
+    return -1;
+  const char* lm = std::getenv("SSIP_POOL_LDS");  // ymax from LDS slots (default) or per-tap selects
+  return !ymax ? 0 : ((lm == nullptr || std::atoi(lm) != 0) ? 2 : 1);
+}
+
+int ssip_stem_bn_pool_kernel_name(int dtype, int N, int H, int W, int C, int k, int s, int pad, int has_ymax,
+                                  char* buf, int buflen) {
+  SSIP_REQUIRE(buf && buflen > 0 && N > 0 && H > 0 && W > 0 && k > 0 && s > 0, SSIP_ERR_ARG,
+               "ssip_stem_bn_pool_kernel_name: bad arguments");
+  const int v = pool_fwd_variant(dtype, H, W, C, k, s, pad, has_ymax != 0);
+  if (v < 0) snprintf(buf, buflen, "stem_bn_pool_fwd<generic>");
+  else snprintf(buf, buflen, "stem_bn_pool_fwd_k3s2<%d>", v);
+  return SSIP_OK;
+}
+
 int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, int pad, const void* y,
                           const float* scale, const float* shift, void* out, uint8_t* idx, void* ymax, void* stream) {
   SSIP_REQUIRE(N > 0 && H > 0 && W > 0 && C % 8 == 0 && 256 % (C / 8) == 0 && k > 0 && k * k <= 255 && s > 0 &&
@@ -485,17 +507,16 @@ int ssip_stem_bn_pool_fwd(int dtype, int N, int H, int W, int C, int k, int s, i
                SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: bad arguments");
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   SSIP_REQUIRE((long)N * H * W * C < (1l << 31), SSIP_ERR_ARG, "ssip_stem_bn_pool_fwd: too large");
-  const char* pr = std::getenv("SSIP_POOL_ROWS");  // pooled rows per workgroup of the k3s2 kernel; 0: generic
-  const int pool_rows = pr ? std::atoi(pr) : 4;
-  if (dtype == SSIP_BF16 && C == 64 && k == 3 && s == 2 && pad == 1 && H % 2 == 0 && W % 2 == 0 &&
-      pool_rows > 0) {
+  const int variant = pool_fwd_variant(dtype, H, W, C, k, s, pad, ymax != nullptr);
+  if (variant >= 0) {
+    const char* pr = std::getenv("SSIP_POOL_ROWS");
+    const int pool_rows = pr ? std::atoi(pr) : 4;
     const int groups = (P + pool_rows - 1) / pool_rows;
     const dim3 grid(N * groups, (Q + 63) / 64), block(Q >= 64 ? 512 : (Q * 8 + 63) / 64 * 64);
-    const char* lm = std::getenv("SSIP_POOL_LDS");  // ymax from LDS slots (default) or per-tap selects
-    if (ymax && (lm == nullptr || std::atoi(lm) != 0))
+    if (variant == 2)
       SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<2>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
                    (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)ymax);
-    else if (ymax)
+    else if (variant == 1)
       SSIP_KLAUNCH(stem_bn_pool_fwd_k3s2_kernel<1>, grid, block, 0, (hipStream_t)stream, H, W, P, Q, pool_rows,
                    (const __bf16*)y, scale, shift, (__bf16*)out, idx, (__bf16*)ymax);
     else

@@ -159,13 +159,20 @@ def load_model(device: torch.device, dtype: str = "fp32", weights: Optional[Path
     return model.to(device)
 
 
+def _as_rgb(img: Image.Image) -> Image.Image:
+    """The reference does not convert (its inputs are RGB: feature_extraction.py
+    :232-240), and its Normalize raises on any other mode.  Both device paths
+    here take Pillow's RGB conversion instead (grayscale replicated, alpha
+    dropped, palettes expanded), so the HIP and --device cpu paths see the
+    same pixels for every file; an RGB file is passed through untouched."""
+    return img if img.mode == "RGB" else img.convert("RGB")
+
+
 def preprocess_image(path: Path) -> np.ndarray:
-    """Decode only (the reference does not convert to RGB: inputs are RGB)."""
+    """Decode to uint8 [H, W, 3] (RGB files as they are, others via _as_rgb)."""
     with Image.open(path) as img:
-        a = np.asarray(img)
-    if a.ndim == 2:
-        a = np.stack([a] * 3, -1)
-    return np.ascontiguousarray(a[..., :3])
+        a = np.asarray(_as_rgb(img))
+    return np.ascontiguousarray(a)
 
 
 def batched(items: Sequence, batch_size: int) -> Iterable[Sequence]:
@@ -177,6 +184,13 @@ def extract_embeddings(records: List[ImageRecord], device: torch.device, batch_s
                        dtype: str = "fp32", weights: Optional[Path] = None,
                        decode_threads: int = 8, allow_random_init: bool = False) -> ExtractionResults:
     if device.type == "cpu":
+        # the host path is the reference's fp32 loop on one process
+        if dtype != "fp32":
+            raise RuntimeError("extract_embeddings: --device cpu computes in fp32 (the reference's precision), "
+                               f"not {dtype}")
+        if D.world() > 1:
+            raise RuntimeError("extract_embeddings: --device cpu runs in one process (torchrun shards the HIP "
+                               "path only: every rank would extract every file and write the same outputs)")
         return _extract_embeddings_host(records, batch_size, weights, decode_threads, allow_random_init)
     model = load_model(device, dtype, weights, allow_random_init)
     tf = build_transform(model.compute_dtype)
@@ -258,7 +272,7 @@ def _extract_embeddings_host(records: List[ImageRecord], batch_size: int, weight
     def load(rec):
         try:
             with Image.open(rec.absolute_path) as img:
-                return rec, pil_extraction_transform(img, TARGET_RESIZE, TARGET_CROP, IMAGENET_MEAN,
+                return rec, pil_extraction_transform(_as_rgb(img), TARGET_RESIZE, TARGET_CROP, IMAGENET_MEAN,
                                                      IMAGENET_STD), None
         except (UnidentifiedImageError, OSError) as exc:
             return rec, None, exc

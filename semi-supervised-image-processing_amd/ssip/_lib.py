@@ -29,7 +29,7 @@ def abi_version_expected() -> int:
     return int(m.group(1)) if m else ABI_VERSION
 
 
-ABI_VERSION = 13  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
+ABI_VERSION = 14  # must equal include/ssip.h SSIP_ABI_VERSION (tests/test_cpu_abi.py)
 
 F32 = 0
 BF16 = 1
@@ -115,6 +115,7 @@ _SIGS = {
     "ssip_bn_bwd_from_partials": (_c_int, [_c_int, _c_i64, _c_int, _c_int] + [_vp] * 8 + [_c_int, _vp, _vp, _vp]),
     "ssip_relu_bwd": (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp]),
     "ssip_stem_bn_pool_fwd": (_c_int, [_c_int] * 8 + [_vp] * 7),
+    "ssip_stem_bn_pool_kernel_name": (_c_int, [_c_int] * 9 + [ctypes.c_char_p, _c_int]),
     "ssip_stem_pool_bn_bwd_partial_floats": (_c_i64, [_c_int] * 4),
     "ssip_stem_pool_bn_bwd": (_c_int, [_c_int] * 8 + [_vp] * 11 + [_c_int] + [_vp] * 4),
     "ssip_maxpool_fwd": (_c_int, [_c_int] * 8 + [_vp, _vp, _vp, _vp]),

@@ -97,6 +97,20 @@ class GradBucketer:
             hi = end if b == 0 else self.ranges[b - 1][0]
             lo = lo if lo == 0 else -(-lo // 4) * 4
             self.ranges[b] = (lo, hi)
+        # What a bucket waits for and whether it launches at all follow the
+        # final ranges, not the parameter lists: a bucket covers every
+        # parameter whose span meets its range (the boundary floats of the
+        # parameter above included), so it launches once all of those are
+        # ready, and whenever any of them trains -- also if its own
+        # parameters are all frozen (those moved floats of a
+        # trainable parameter were otherwise never reduced).
+        self.covers: List[List[int]] = []
+        for lo, hi in self.ranges:
+            self.covers.append([i for i, (o, n) in enumerate(spans) if n > 0 and o < hi and o + n > lo])
+        self.buckets_of = {}
+        for b, idxs in enumerate(self.covers):
+            for i in idxs:
+                self.buckets_of.setdefault(id(params[i]), []).append(b)
         # hipGraph mode (SemiStep(graph=True)): the backward is captured
         # without collectives (ROCm allows no external event nodes in a graph,
         # so a bucket cannot signal mid-replay); after each replay
@@ -114,8 +128,12 @@ class GradBucketer:
             self._op = dist._make_nccl_premul_sum(self.premul)
         return self._op
 
+    def trains(self, b: int) -> bool:
+        """Bucket b holds gradient elements of a trainable parameter."""
+        return any(self.params[i].requires_grad for i in self.covers[b])
+
     def reset(self):
-        self.pending = [set(i for i in idxs if self.params[i].requires_grad) for idxs in self.buckets]
+        self.pending = [set(i for i in idxs if self.params[i].requires_grad) for idxs in self.covers]
         self.handles = []
         self.launched = [False] * len(self.buckets)
 
@@ -142,7 +160,7 @@ class GradBucketer:
         self._comm.wait_stream(torch.cuda.current_stream())
         self.handles = []
         for b in range(len(self.buckets)):
-            if self.active and any(self.params[i].requires_grad for i in self.buckets[b]):
+            if self.active and self.trains(b):
                 lo, hi = self.ranges[b]
                 with torch.cuda.stream(self._comm):
                     self.handles.append(dist.all_reduce(self.arena.grad[lo:hi], op=self._reduce_op(),
@@ -152,12 +170,10 @@ class GradBucketer:
     def mark_ready(self, params) -> None:
         idx = {id(p): i for i, p in enumerate(self.params)}
         for p in params:
-            b = self.bucket_of.get(id(p))
-            if b is None:
-                continue
-            self.pending[b].discard(idx[id(p)])
-            if not self.pending[b]:
-                self._launch(b)
+            for b in self.buckets_of.get(id(p), ()):
+                self.pending[b].discard(idx[id(p)])
+                if not self.pending[b] and self.trains(b):
+                    self._launch(b)
 
     def grad_scale(self) -> float:
         """The factor AdamW applies to the reduced gradients: the 1/world
@@ -167,7 +183,7 @@ class GradBucketer:
     def finish(self) -> float:
         """Launch anything left, wait, and return the grad scale (1 / (world * premul))."""
         for b in range(len(self.buckets)):
-            if any(self.params[i].requires_grad for i in self.buckets[b]):
+            if self.trains(b):
                 self._launch(b)
         for h in self.handles:
             h.wait()

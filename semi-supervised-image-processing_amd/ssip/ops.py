@@ -539,6 +539,13 @@ def stem_bn_pool_fwd(N, H, W, C, k, s, pad, y, scale, shift, out, idx, ymax=None
          _p(idx), _p(ymax), stream_ptr())
 
 
+def stem_bn_pool_kernel_name(dtype: torch.dtype, N, H, W, C, k, s, pad, has_ymax: bool) -> str:
+    """The kernel stem_bn_pool_fwd launches for this shape (ssip_stem_bn_pool_kernel_name, ABI 14)."""
+    buf = ctypes.create_string_buffer(96)
+    call("ssip_stem_bn_pool_kernel_name", _DT[dtype], N, H, W, C, k, s, pad, int(has_ymax), buf, 96)
+    return buf.value.decode()
+
+
 def stem_pool_bn_bwd_partial_floats(N, H, W, C) -> int:
     return int(_lib.lib().ssip_stem_pool_bn_bwd_partial_floats(N, H, W, C))
 

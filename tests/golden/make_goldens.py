@@ -8,7 +8,8 @@ delegates every image op to Pillow exactly as torchvision does.  Nothing in
 this script runs on the GPU box (it needs /root/reference); the fixtures it
 writes are small data files (inputs and expected outputs).
 
-Run:  python tests/golden/make_goldens.py
+Run:  python tests/golden/make_goldens.py            (everything)
+      python tests/golden/make_goldens.py --only real  (section 11 only)
 """
 from __future__ import annotations
 
@@ -37,6 +38,12 @@ def main() -> None:
     from training import common as C  # reference module
     from training import semi_supervised as SS  # reference module
     import src.feature_extraction as FE  # reference module
+
+    # 11. the reference's run_supervised on its own labelled MRI set at 224^2
+    #     (prediction-level parity on the real val/test split)
+    _real_supervised(C)
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "real":
+        return
 
     data = REF / "mri_dataset_brain_cancer_oc"
     goldens = {}
@@ -305,6 +312,82 @@ def _pipelines(C, SS) -> dict:
             os.environ.pop("SSIP_RESNET18_WEIGHTS", None)
             SS.generate_pseudo_labels = real
     return res
+
+
+REAL_CFG = dict(batch_size=16, image_size=224, num_workers=2, baseline_epochs=10, target_recall=0.98,
+                min_precision=0.60, seed=42)
+REAL_DIR = OUT / "mri_avec_labels"
+
+
+def _real_supervised(C) -> None:
+    """Section 11: the reference's own run_supervised on the 100 labelled JPEGs
+    of mri_dataset_brain_cancer_oc/avec_labels (shipped as fixture data under
+    tests/golden/mri_avec_labels/, 2.8 MB, the same file names so the
+    ImageFolder order and the stratified split are the reference's) at its
+    defaults (batch 16, 224^2, 2 loader workers, 10 baseline epochs, early
+    stopping 3) with the threshold policy of its report
+    (notes/training_report.md: --target-recall 0.98 --min-precision 0.60),
+    the seeded stand-in for the ImageNet weights.  Records every metric and
+    evaluate_model call per sample (_PredRecorder) and the history; written to
+    tests/golden/real_supervised.json."""
+    import os
+    import shutil
+
+    import torch
+
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(OUT))
+    import tiny_dataset
+    from training import supervised as SV  # reference module
+
+    src = REF / "mri_dataset_brain_cancer_oc" / "avec_labels"
+    for cls in ("cancer", "normal"):
+        (REAL_DIR / cls).mkdir(parents=True, exist_ok=True)
+        for f in sorted((src / cls).iterdir()):
+            dst = REAL_DIR / cls / f.name
+            if not dst.exists():
+                shutil.copyfile(f, dst)
+    cwd = os.getcwd()
+    rec = _PredRecorder()
+    real_fns = {(mod, nm): getattr(mod, nm) for mod in (C, SV)
+                for nm in ("create_model", "compute_accuracy_f1", "evaluate_model") if hasattr(mod, nm)}
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        wpath = td / "w.pt"
+        torch.save(tiny_dataset.pretrained_state_dict(1234), wpath)
+        os.environ["SSIP_RESNET18_WEIGHTS"] = str(wpath)
+        hist = {}
+        real_train = SV.train_model
+
+        def train_model(*a, **k):
+            model, h = real_train(*a, **k)
+            hist.update(h)
+            return model, h
+
+        try:
+            for (mod, nm), fn in real_fns.items():
+                setattr(mod, nm, {"create_model": rec.wrap_create, "compute_accuracy_f1": rec.wrap_metric,
+                                  "evaluate_model": rec.wrap_eval}[nm](fn))
+            SV.train_model = train_model
+            os.chdir(td)
+            cfg = C.TrainingConfig(strong_data_dir=REAL_DIR, weak_data_dir=REAL_DIR, device="cpu", **REAL_CFG)
+            metrics = SV.run_supervised(cfg)
+            for m in metrics.values():
+                m["training_time_sec"] = None
+            art = _read_artifacts(td / "outputs", False)
+        finally:
+            for (mod, nm), fn in real_fns.items():
+                setattr(mod, nm, fn)
+            SV.train_model = real_train
+            os.chdir(cwd)
+            os.environ.pop("SSIP_RESNET18_WEIGHTS", None)
+    res = {"config": REAL_CFG, "weights_seed": 1234, "data": str(src.relative_to(REF)),
+           "metrics": json.loads(json.dumps(metrics, default=float)), "artifacts": art,
+           "history": json.loads(json.dumps(hist, default=float)),
+           "metric_calls": rec.metric_calls, "eval_calls": rec.eval_calls}
+    with open(OUT / "real_supervised.json", "w") as f:
+        json.dump(res, f, indent=1, default=float)
+    print("wrote real_supervised.json:", len(rec.metric_calls), "metric calls,", len(rec.eval_calls), "eval calls")
 
 
 class _PredRecorder:

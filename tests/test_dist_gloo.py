@@ -206,6 +206,88 @@ def test_bucket_ranges_cover_arena_in_multiples_of_four():
             cover[lo:hi] += 1
             owner[lo:hi] = b
         assert int(cover.min()) == 1 and int(cover.max()) == 1
+        for trainable in (None, {"fc.weight", "fc.bias"}):
+            names = {id(p): n for n, p in m.named_parameters()}
+            for p in ar.params:
+                p.requires_grad_(trainable is None or names[id(p)] in trainable)
+            _check_bucket_launches(bk, ar)
         for p in ar.params:
-            off, n = ar.span(p)
-            assert int(owner[off:off + n].min()) >= bk.bucket_of[id(p)]
+            p.requires_grad_(True)
+
+
+class _OddArena:
+    """An arena stand-in whose parameter spans are not multiples of 4 floats,
+    so GradBucketer's rounded boundaries move floats between buckets."""
+
+    def __init__(self, sizes):
+        import torch
+
+        self.params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+        self._off = {}
+        o = 0
+        for p, n in zip(self.params, sizes):
+            self._off[id(p)] = (o, n)
+            o += n
+        self.numel = o
+        self.padded = -(-o // 64) * 64
+        self.grad = torch.zeros(self.padded)
+
+    def span(self, p):
+        return self._off[id(p)]
+
+
+def _check_bucket_launches(bk, ar):
+    """Backward order (last parameter first), one mark_ready per trainable
+    parameter (the engine hooks only what it computes gradients for): every element of a trainable parameter lies in a bucket that launches,
+    and a bucket launches only once every trainable parameter whose span
+    meets its range is ready (a bucket of frozen parameters still
+    carries the boundary floats of a trainable one above it)."""
+    ready = set()
+    launches = {}
+    real = bk._launch
+
+    def spy(b):
+        if not bk.launched[b]:
+            launches[b] = set(ready)
+        real(b)
+
+    bk._launch = spy
+    try:
+        bk.reset()
+        for i in range(len(bk.params) - 1, -1, -1):
+            if bk.params[i].requires_grad:
+                ready.add(i)
+                bk.mark_ready([bk.params[i]])
+        bk.finish()
+    finally:
+        bk._launch = real
+    for i, p in enumerate(bk.params):
+        off, n = ar.span(p)
+        for b, (lo, hi) in enumerate(bk.ranges):
+            if off < hi and off + n > lo and p.requires_grad:
+                assert b in launches, ("bucket with trainable floats never launched", b, i)
+                assert i in launches[b], ("bucket launched before a parameter it carries was ready", b, i)
+
+
+def test_bucket_launches_cover_trainable_boundary_floats():
+    """Odd spans: every boundary is rounded up, so the lowest floats of a
+    bucket's lowest parameter belong to the bucket below.  With that bucket's
+    own parameters all frozen it must still launch (and wait for the
+    trainable parameter above)."""
+    from ssip.dist import GradBucketer
+
+    ar = _OddArena([6, 3, 5, 10, 7, 9, 2, 13])
+    for bb in (24, 40, 60):
+        bk = GradBucketer(ar, bucket_bytes=bb)
+        assert len(bk.ranges) >= 2
+        moved = [b for b in range(1, len(bk.ranges))
+                 if min(ar.span(bk.params[i])[0] for i in bk.buckets[b - 1]) % 4]
+        assert moved, "the case needs a rounded boundary"
+        for b in range(len(bk.buckets)):  # bucket b's own parameters frozen, the rest trainable
+            for i, p in enumerate(ar.params):
+                p.requires_grad_(i not in bk.buckets[b])
+            _check_bucket_launches(bk, ar)
+        for keep in range(len(ar.params)):  # one trainable parameter at a time
+            for i, p in enumerate(ar.params):
+                p.requires_grad_(i == keep)
+            _check_bucket_launches(bk, ar)

@@ -225,3 +225,125 @@ def test_stem_bs256(dev):
     scale_w1 = ref_w1.abs().max().item()
     assert (dw0.cpu() - ref_w1).abs().max().item() <= 1e-4 * scale_w1
     assert (dw1.cpu() - ref_w1).abs().max().item() <= 2e-3 * scale_w1
+
+
+def _bn_affine(C, gen):
+    """A BatchNorm affine of both signs (scale = gamma * invstd, shift = beta - mean * scale)."""
+    scale = (torch.rand(C, generator=gen) + 0.25) * torch.where(torch.rand(C, generator=gen) < 0.2, -1.0, 1.0)
+    shift = torch.randn(C, generator=gen) * 0.5
+    return scale, shift
+
+
+def _bnrelu_ref(y, scale, shift):
+    """bf16(relu(fma_f32(y, scale, shift))), NCHW: ssip_bn_apply's arithmetic.
+    The product of a bf16 y and an fp32 scale is exact in fp64 and the sum is
+    rounded to fp64 once, so rounding that to fp32 is the fp32 fma (up to a
+    double-rounding case of probability ~2^-29); then one RNE rounding to bf16."""
+    z = (y.double() * scale.double()[None, :, None, None] + shift.double()[None, :, None, None]).float()
+    return torch.relu(z).bfloat16().float()
+
+
+@pytest.mark.parametrize("n", [N, 128], ids=["bs256", "weak128"])
+def test_bnrelu_in_fwd_bench_geometry(dev, n):
+    """ABI 13's layer-1 forward with bn1's BN+ReLU formed in the conv's LDS
+    tile (the step's layer1.x.conv2 at batch 256; the weak forward's 128),
+    against torch fp32 conv2d of relu(bn(y1)) on bf16-rounded operands, plus
+    its BN statistics and the optional z_out."""
+    C = K = 64
+    H = 56
+    g = _geom(C, H, K, 3, 1, 1, n=n)
+    assert ops.conv_bnrelu_in_supported(g, DT)
+    assert ops.conv_kernel_name("fwd", g, DT).startswith("halo<fwd"), ops.conv_kernel_name("fwd", g, DT)
+    gen = torch.Generator().manual_seed(104)
+    y1 = _rnd(torch.randn(n, C, H, H, generator=gen))
+    scale, shift = _bn_affine(C, gen)
+    w = _rnd(torch.randn(K, C, 3, 3, generator=gen) * (2.0 / (C * 9)) ** 0.5)
+    z = _bnrelu_ref(y1, scale, shift)
+    ref = F.conv2d(z, w, stride=1, padding=1)
+    yh = ops.nchw_to_nhwc(y1.to(dev), C, DT)
+    krsc = torch.empty((K, 3, 3, C), device=dev, dtype=DT)
+    ops.weight_prep(w.to(dev), DT, C, 3, krsc, None)
+    out = torch.empty((n, H, H, K), device=dev, dtype=DT)
+    part = torch.full((ops.conv_fwd_partial_floats(g),), float("nan"), device=dev)
+    zo = torch.empty_like(yh)
+    ops.conv_fwd_bnrelu_in(g, yh, scale.to(dev), shift.to(dev), krsc, out, part, z_out=zo)
+    stats = torch.empty((4, K), device=dev)
+    rm, rv = torch.zeros(K, device=dev), torch.ones(K, device=dev)
+    ops.bn_finalize(K, ops.conv_fwd_partial_tiles(g, DT), part, torch.ones(K, device=dev), torch.zeros(K, device=dev),
+                    rm, rv, 0.1, 1e-5, True, stats[0], stats[1], stats[2], stats[3])
+    torch.cuda.synchronize()
+    _check_bf16(out, ref, f"bnrelu_in fwd n={n}")
+    # z_out: the transformed input itself, bit for bit
+    assert torch.equal(zo.float().cpu(), z.permute(0, 2, 3, 1))
+    r = ref.double().permute(0, 2, 3, 1).reshape(-1, K)
+    mean, var = r.mean(0), r.var(0, unbiased=False)
+    assert ((stats[0].cpu().double() - mean).abs().max() / var.sqrt().max()).item() < 1e-3
+    assert ((1.0 / stats[1].cpu().double() ** 2 - 1e-5 - var).abs().max() / var.max()).item() < 1e-3
+
+
+def test_bnrelu_in_wgrad_bench_geometry(dev):
+    """ABI 13's layer-1 weight gradient with the input relu(bn(y1)) formed in
+    LDS, at batch 256: the full grid and the step's side-stream budget (half the
+    CUs), fresh and accumulating, against torch fp32 conv2d_weight."""
+    from ssip.resnet import _side_wgrad_budget
+
+    C = K = 64
+    H = 56
+    g = _geom(C, H, K, 3, 1, 1)
+    assert ops.conv_bnrelu_in_supported(g, DT)
+    assert ops.conv_kernel_name("wgrad", g, DT).startswith("halo_wgrad<"), ops.conv_kernel_name("wgrad", g, DT)
+    gen = torch.Generator().manual_seed(105)
+    y1 = _rnd(torch.randn(N, C, H, H, generator=gen))
+    scale, shift = _bn_affine(C, gen)
+    dy = _rnd(torch.randn(N, K, H, H, generator=gen) * 1e-2)
+    z = _bnrelu_ref(y1, scale, shift)
+    ref = torch.nn.grad.conv2d_weight(z, (K, C, 3, 3), dy, stride=1, padding=1)
+    yh = ops.nchw_to_nhwc(y1.to(dev), C, DT)
+    dyh = ops.nchw_to_nhwc(dy.to(dev), K, DT)
+    sc, sh = scale.to(dev), shift.to(dev)
+    scale_max = ref.abs().max().item()
+    base = torch.randn(K, C, 3, 3, device=dev)
+    for b in (0, _side_wgrad_budget(g, DT, dev)):
+        ws = torch.empty(ops.conv_wgrad_workspace_bytes(g, b), device=dev, dtype=torch.uint8)
+        dw = torch.full((K, C, 3, 3), float("nan"), device=dev)
+        ops.conv_wgrad_bnrelu_in(g, dyh, yh, sc, sh, dw, False, ws, max_workgroups=b)
+        dwa = base.clone()
+        ops.conv_wgrad_bnrelu_in(g, dyh, yh, sc, sh, dwa, True, ws, max_workgroups=b)
+        torch.cuda.synchronize()
+        assert (dw.cpu() - ref).abs().max().item() <= 1e-4 * scale_max, b
+        assert (dwa.cpu() - base.cpu() - ref).abs().max().item() <= 1e-4 * scale_max + 1e-6 * base.abs().max().item(), b
+
+
+@pytest.mark.parametrize("n,ymax", [(N, True), (128, False)], ids=["bs256_ymax", "weak128"])
+def test_stem_pool_k3s2_bench_geometry(dev, n, ymax):
+    """The stem's BN+ReLU+3x3/2 max-pool (stem_bn_pool_fwd_k3s2) at 112^2:
+    batch 256 with argmax + ymax (the train forward), batch 128 without ymax
+    (the weak forward), against torch fp32 max_pool2d of relu(bn(y)) --
+    pooled values exact, argmax = torch's window index, ymax = y there."""
+    C, H = 64, 112
+    want = f"stem_bn_pool_fwd_k3s2<{2 if ymax else 0}>"
+    assert ops.stem_bn_pool_kernel_name(DT, n, H, H, C, 3, 2, 1, ymax) == want
+    gen = torch.Generator().manual_seed(106)
+    y = _rnd(torch.randn(n, C, H, H, generator=gen))
+    scale, shift = _bn_affine(C, gen)
+    z = _bnrelu_ref(y, scale, shift)
+    ref, ridx = F.max_pool2d(z, 3, 2, 1, return_indices=True)
+    yh = ops.nchw_to_nhwc(y.to(dev), C, DT)
+    P = 56
+    out = torch.empty(n, P, P, C, device=dev, dtype=DT)
+    idx = torch.empty(n, P, P, C, device=dev, dtype=torch.uint8)
+    ym = torch.empty(n, P, P, C, device=dev, dtype=DT) if ymax else None
+    ops.stem_bn_pool_fwd(n, H, H, C, 3, 2, 1, yh, scale.to(dev), shift.to(dev), out, idx, ym)
+    torch.cuda.synchronize()
+    got = out.float().cpu().permute(0, 3, 1, 2)
+    assert torch.equal(got, ref)
+    # argmax bytes (window tap t = 3 dr + ds) -> the flat input index torch
+    # returns; both take the first maximum in window order
+    t = idx.long().cpu().permute(0, 3, 1, 2)
+    pr = torch.arange(P).view(1, 1, P, 1)
+    pc = torch.arange(P).view(1, 1, 1, P)
+    flat = (2 * pr - 1 + t // 3) * H + (2 * pc - 1 + t % 3)
+    assert torch.equal(flat, ridx)
+    if ymax:
+        yv = y.reshape(n, C, H * H).gather(2, ridx.reshape(n, C, -1)).reshape(n, C, P, P)
+        assert torch.equal(ym.float().cpu().permute(0, 3, 1, 2), yv)

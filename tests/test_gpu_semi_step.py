@@ -362,3 +362,52 @@ def test_early_adamw_matches_one_update(dev, monkeypatch, plan):
     assert torch.equal(w0, w1)
     for a, b in zip(s0, s1):
         assert torch.equal(a, b)
+
+
+def _bf16_steps(dev, seed_data, n=3, S=64, B=8, plan=False):
+    g = torch.Generator().manual_seed(seed_data)
+    x_l = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    x_u = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    y_l = torch.randint(0, 2, (B,), generator=g).to(dev)
+    torch.manual_seed(0)
+    m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2).to(dev).train()
+    step = SemiStep(m, lr=1e-3, weight_decay=1e-4, tau=0.5, image_size=S, seed=13, plan=plan)
+    losses = [step(x_l, y_l, x_u).loss.clone() for _ in range(n)]
+    torch.cuda.synchronize()
+    return torch.stack(losses).cpu(), step.arena.flat.detach().cpu().clone()
+
+
+def test_bnrelu_in_step_bit_identical(dev, monkeypatch):
+    """layer 1's BN+ReLU applied inside the next conv
+    (SSIP_BNRELU_IN, the default) and its z_out wiring (SSIP_BNRELU_Z: the
+    forward writes relu(bn(y1)) and the backward runs the plain halo wgrad on
+    it) give the same losses and weights, bit for bit, as the separate apply
+    pass, over 3 SemiSteps (forward, backward and AdamW)."""
+    from ssip import ops
+    from ssip import resnet as R
+
+    S, B = 64, 8
+    m = replace_fc(SSIPResNet("resnet18", 1000, dtype="bf16"), 2)
+    assert ops.conv_bnrelu_in_supported(R._geom(m.layer1[0].conv2, 2 * B, S // 4, S // 4), torch.bfloat16)
+    runs = []
+    for bn_in, bn_z in ((False, False), (True, False), (True, True)):
+        monkeypatch.setattr(R, "_BNRELU_IN", bn_in)
+        monkeypatch.setattr(R, "_BNRELU_Z", bn_z)
+        runs.append(_bf16_steps(dev, 21, S=S, B=B))
+    for l, w in runs[1:]:
+        assert torch.equal(l, runs[0][0])
+        assert torch.equal(w, runs[0][1])
+
+
+@pytest.mark.parametrize("plan", [False, True])
+def test_conv_stagger_step_bit_identical(dev, monkeypatch, plan):
+    """The conv k-loop stagger (SSIP_STAGGER: waves NW/2.. run each k-step's
+    second MFMA half after the next barrier) keeps every accumulation in the
+    same order: 3 SemiSteps give the same losses and weights, bit for bit,
+    with it off and on for every pass."""
+    runs = []
+    for st in ("0", "7"):
+        monkeypatch.setenv("SSIP_STAGGER", st)
+        runs.append(_bf16_steps(dev, 22, S=96, B=16, plan=plan))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])

@@ -35,6 +35,14 @@ def _dataset(root: Path, n_per_class=4, n_unl=6, size=96):
         a = np.clip(rng.normal(120, 50, (size + 8 * i, size, 3)), 0, 255).astype(np.uint8)
         Image.fromarray(a).save(u / f"u_{i:03d}.jpg", quality=90)
     (u / "broken.jpg").write_bytes(b"not a jpeg")  # a decode failure is logged and skipped
+    # non-RGB files: grayscale, RGBA and palette PNGs take Pillow's
+    # RGB conversion on both device paths
+    g = np.clip(rng.normal(110, 40, (size, size + 8)), 0, 255).astype(np.uint8)
+    Image.fromarray(g, "L").save(u / "v_gray.png")
+    rgba = np.clip(rng.normal(140, 40, (size + 4, size, 4)), 0, 255).astype(np.uint8)
+    Image.fromarray(rgba, "RGBA").save(u / "v_rgba.png")
+    Image.fromarray(np.clip(rng.normal(100, 60, (size, size, 3)), 0, 255).astype(np.uint8)).quantize(16).save(
+        u / "v_pal.png")
     return root
 
 
@@ -70,14 +78,41 @@ def test_cli_device_cpu(tmp_path, monkeypatch):
 
     FE.main(["--data-dir", str(data), "--device", "cpu", "--batch-size", "32", "--random-init"])
     emb = np.load(tmp_path / "outputs/features/embeddings.npy")
-    assert emb.shape == (14, 512) and emb.dtype == np.float32 and np.isfinite(emb).all()
+    assert emb.shape == (17, 512) and emb.dtype == np.float32 and np.isfinite(emb).all()
     meta = json.loads((tmp_path / "outputs/features/metadata.json").read_text())
     gm = json.loads((GOLD_DIR / "goldens.json").read_text())["committed_metadata"]
-    assert meta["device"] == "cpu" and meta["num_images"] == 14 and meta["failed_images"] == 1
+    assert meta["device"] == "cpu" and meta["num_images"] == 17 and meta["failed_images"] == 1
     for k in gm["keys"]:
         assert k in meta, k
     for f in ("features/embeddings.csv", "logs/feature_extraction.log", "notes/feature_summary.md"):
         assert (tmp_path / "outputs" / f).exists(), f
+
+
+def test_non_rgb_inputs_take_the_rgb_conversion(tmp_path):
+    """Both device paths decode through the same RGB conversion: the HIP
+    path's uint8 input is Pillow's convert('RGB') of every non-RGB file."""
+    from src import feature_extraction as FE
+
+    data = _dataset(tmp_path / "mri", n_per_class=1, n_unl=1)
+    for nm in ("v_gray.png", "v_rgba.png", "v_pal.png"):
+        f = data / "sans_label" / nm
+        with Image.open(f) as im:
+            assert im.mode != "RGB"
+            want = np.asarray(im.convert("RGB"))
+        got = FE.preprocess_image(f)
+        assert got.shape == want.shape and got.dtype == np.uint8 and np.array_equal(got, want), nm
+
+
+def test_host_path_refuses_bf16_and_world(monkeypatch, tmp_path):
+    from src import feature_extraction as FE
+    from src.training import distributed as D
+
+    recs = FE.discover_image_records(_dataset(tmp_path / "mri", n_per_class=1, n_unl=1))
+    with pytest.raises(RuntimeError, match="fp32"):
+        FE.extract_embeddings(recs, torch.device("cpu"), dtype="bf16", allow_random_init=True)
+    monkeypatch.setattr(D, "world", lambda: 2)
+    with pytest.raises(RuntimeError, match="one process"):
+        FE.extract_embeddings(recs, torch.device("cpu"), allow_random_init=True)
 
 
 @pytest.mark.gpu

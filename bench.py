@@ -82,6 +82,9 @@ def parse():
                     help="profiling run (no JSON line): warm-up, then --steps repetitions of that roofline leg "
                          "alone, without event timers, for rocprofv3 --kernel-trace / --pmc "
                          "(tools/roofline_from_trace.py takes the last complete step)")
+    ap.add_argument("--sclk-out", default=None,
+                    help="--profile-leg: write the legs' mean SCLK (amdsmi, the bench line's sampler) to this JSON "
+                         "file, so a trace's MFMA busy is normalised by its own box's clock")
     ap.add_argument("--max-inflight", type=int, default=None,
                     help="host waits for step k - N before enqueueing step k (0: never; default: SemiStep's own "
                          "bound on launch-plan replays, $SSIP_MAX_INFLIGHT or 2)")
@@ -302,11 +305,16 @@ def main():
     for _ in range(args.warmup):
         step(x_l, y_l, x_u)
     if args.profile_leg:
-        for _ in range(args.steps):
-            # every step of the trace after the warm-up is a leg step (no lead-in
-            # replays): the profile tools take the last complete one
-            roofline_leg(step, x_l, y_l, x_u, args.profile_leg, ops, resnet_mod, timer=False, lead=0)
-        print(f"profile-leg {args.profile_leg}: {args.steps} legs done", file=sys.stderr)
+        with SclkSampler(local) as sclk:
+            for _ in range(args.steps):
+                # every step of the trace after the warm-up is a leg step (no lead-in
+                # replays): the profile tools take the last complete one
+                roofline_leg(step, x_l, y_l, x_u, args.profile_leg, ops, resnet_mod, timer=False, lead=0)
+        sc = sclk.summary()
+        print(f"profile-leg {args.profile_leg}: {args.steps} legs done; sclk {json.dumps(sc)}", file=sys.stderr)
+        if args.sclk_out:
+            with open(args.sclk_out, "w") as f:
+                json.dump({"leg": args.profile_leg, "steps": args.steps, "sclk": sc}, f)
         return
     slots = step.input_slots()
     if slots is not None and os.environ.get("SSIP_NO_INPUT_SLOTS") != "1":

@@ -3078,11 +3078,15 @@ static int apply_force(int mode, int elem_bytes, Plan& pl) {
 // SSIP_STAGGER (read per plan, so a lab can flip it in one process): a
 // bit mask over the passes whose LDS-DMA ring kernels run the stagger
 // (conv_glds_kernel: waves NW/2.. one MFMA half behind), 1 fwd, 2 dgrad,
-// 4 wgrad; 0 off.
+// 4 wgrad; 0 off; default 7 (round 6, tools/stagger_lab.py, batch 256, same
+// bits: the layer 2-4 launches -3.8 % in sum, the 256x256 layer-3 fwd /
+// dgrad -11 to -13 %, the side stream's one-workgroup-per-CU wgrads -4 to
+// -6 %; step 6.076 -> 6.045 ms, 3 + 3 alternated runs,
+// profiles/r6_stagger_lab.txt).
 static int stagger_for(int mode, const Plan& pl) {
   if (pl.stages <= 0 || pl.conv1) return 0;
   const char* e = getenv("SSIP_STAGGER");
-  const int m = e != nullptr ? atoi(e) : 0;
+  const int m = e != nullptr ? atoi(e) : 7;
   return (m >> mode) & 1;
 }
 

@@ -347,6 +347,25 @@ def _real_supervised(C) -> None:
             dst = REAL_DIR / cls / f.name
             if not dst.exists():
                 shutil.copyfile(f, dst)
+    res = _run_supervised_recorded(C, SV, tiny_dataset)
+    # the reference's own run-to-run spread on this set: the same run with
+    # torch's CPU convolutions on its non-mkldnn algorithms (another fp32
+    # summation order, nothing else changed) -- the yardstick for how far any
+    # fp32 implementation's probabilities drift over these AdamW steps
+    with torch.backends.mkldnn.flags(enabled=False):
+        alt = _run_supervised_recorded(C, SV, tiny_dataset)
+    res["alt_no_mkldnn"] = {k: alt[k] for k in ("history", "metric_calls", "eval_calls", "metrics")}
+    res.update({"config": REAL_CFG, "weights_seed": 1234, "data": str(src.relative_to(REF))})
+    with open(OUT / "real_supervised.json", "w") as f:
+        json.dump(res, f, indent=1, default=float)
+    print("wrote real_supervised.json:", len(res["metric_calls"]), "metric calls,", len(res["eval_calls"]), "eval calls")
+
+
+def _run_supervised_recorded(C, SV, tiny_dataset) -> dict:
+    import os
+
+    import torch
+
     cwd = os.getcwd()
     rec = _PredRecorder()
     real_fns = {(mod, nm): getattr(mod, nm) for mod in (C, SV)
@@ -381,13 +400,9 @@ def _real_supervised(C) -> None:
             SV.train_model = real_train
             os.chdir(cwd)
             os.environ.pop("SSIP_RESNET18_WEIGHTS", None)
-    res = {"config": REAL_CFG, "weights_seed": 1234, "data": str(src.relative_to(REF)),
-           "metrics": json.loads(json.dumps(metrics, default=float)), "artifacts": art,
-           "history": json.loads(json.dumps(hist, default=float)),
-           "metric_calls": rec.metric_calls, "eval_calls": rec.eval_calls}
-    with open(OUT / "real_supervised.json", "w") as f:
-        json.dump(res, f, indent=1, default=float)
-    print("wrote real_supervised.json:", len(rec.metric_calls), "metric calls,", len(rec.eval_calls), "eval calls")
+    return {"metrics": json.loads(json.dumps(metrics, default=float)), "artifacts": art,
+            "history": json.loads(json.dumps(hist, default=float)),
+            "metric_calls": rec.metric_calls, "eval_calls": rec.eval_calls}
 
 
 class _PredRecorder:

@@ -316,3 +316,145 @@ def test_semi_step_dp2_bench_geometry(dev, tmp_path):
     for k in ("y_pred", "y_prob", "paths", "picks"):
         assert r[0][k] == single[k], k
         assert r[1][k] == single[k], k
+
+
+_BWD = ("dgrad", "wgrad")
+
+
+def _overlap_worker(rank, world, port, out):
+    """Eager steps, then a plan recording and replays, logging host-side order:
+    every C-ABI launch (eager) / every plan segment's launches (replay) and
+    every bucket all-reduce launch."""
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "semi-supervised-image-processing_amd"), str(root)]
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ssip import _lib, ops
+        from ssip import plan as P
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        step = _make(dev, bucketer_world=True, plan=True)
+        bk = step.bucketer
+        log = []            # eager: ("call", name) / ("ar", bucket)
+        seg_names = [[]]    # plan recording: launch names per segment
+        cur = {"seg": None}  # plan replay: the segment whose callback is running
+
+        real_call = _lib.call
+
+        def call(name, *a):
+            log.append(("call", name))
+            return real_call(name, *a)
+
+        _lib.call = ops.call = call
+        real_on_call, real_cb = P.PlanRecorder.on_call, P.PlanRecorder.callback
+
+        def on_call(self, name, args):
+            seg_names[-1].append(name)
+            return real_on_call(self, name, args)
+
+        def callback(self, fn, args):
+            seg_names.append([])
+            return real_cb(self, fn, args)
+
+        P.PlanRecorder.on_call, P.PlanRecorder.callback = on_call, callback
+
+        def replay(self):
+            lib = _lib.lib()
+            for seg in range(self.segments):
+                _lib.check(lib.ssip_plan_run(self.handle, seg), "ssip_plan_run")
+                if seg < len(self.callbacks):
+                    cur["seg"] = seg
+                    fn, args = self.callbacks[seg]
+                    fn(*args)
+                    cur["seg"] = None
+
+        P.Plan.replay = replay
+        real_launch = bk._launch
+
+        def launch(b):
+            if not bk.launched[b]:
+                log.append(("ar", b, cur["seg"]))
+            return real_launch(b)
+
+        bk._launch = launch
+        real_reset = bk.reset
+
+        def reset():
+            log.append(("reset",))
+            return real_reset()
+
+        bk.reset = reset
+        x_l, y_l, x_u, params = _data(rank)
+        x_l, y_l, x_u = x_l.to(dev), y_l.to(dev), x_u.to(dev)
+        for i in range(STEPS):
+            step(x_l, y_l, x_u, params[i])
+        torch.cuda.synchronize()
+        assert step._plan is not None
+        torch.save({"log": log, "seg_names": seg_names, "nbuckets": len(bk.buckets),
+                    "trains": [bk.trains(b) for b in range(len(bk.buckets))]},
+                   os.path.join(out, f"overlap{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_overlaps_backward(dev, tmp_path):
+    """north_star's "RCCL gradient all-reduce ... overlapped with backward" as a
+    tested property (the loop being sharded: reference
+    src/training/common.py:376-387).  2 ranks over gloo, SemiStep with 8 MiB
+    buckets, eager steps and launch-plan replays: every bucket's all-reduce
+    but the last is enqueued while backward work (a dgrad or wgrad launch) is
+    still to be enqueued after it in the same step -- in eager steps counted in
+    C-ABI launches, in plan replays in plan segments (the bucket launches from
+    the callback after segment k; a later segment must still hold a dgrad /
+    wgrad)."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(200)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank in (0, 1):
+        r = torch.load(tmp_path / f"overlap{rank}.pt", weights_only=False)
+        log, seg_names, nb = r["log"], r["seg_names"], r["nbuckets"]
+        assert nb >= 3 and all(r["trains"])
+        # one step per bucketer reset (eager steps, the recording step and
+        # every replay reset it first)
+        steps, cur_step = [], None
+        for e in log:
+            if e[0] == "reset":
+                cur_step = []
+                steps.append(cur_step)
+            elif cur_step is not None:
+                cur_step.append(e)
+        eager_steps = checked_replays = 0
+        for part in steps:
+            ars = [(k, e) for k, e in enumerate(part) if e[0] == "ar"]
+            if not ars:
+                continue
+            assert len(ars) == nb, (rank, "every bucket launches once per step", len(ars))
+            if all(e[2] is None for _, e in ars):  # eager (or the recording step): C-ABI launches logged
+                eager_steps += 1
+                for k, e in ars[:-1]:
+                    later = [x[1] for x in part[k + 1:] if x[0] == "call"]
+                    assert any(t in n for n in later for t in _BWD), \
+                        (rank, "bucket all-reduce enqueued after the backward's last launch", e[1])
+            else:  # a replay: bucket launches from the callbacks between plan segments
+                checked_replays += 1
+                for _, e in ars[:-1]:
+                    assert e[2] is not None
+                    later = [n for sg in seg_names[e[2] + 1:] for n in sg]
+                    assert any(t in n for n in later for t in _BWD), \
+                        (rank, "bucket all-reduce launched after the backward's final segment", e[1], e[2])
+        assert eager_steps >= 2 and checked_replays >= 1, (rank, eager_steps, checked_replays)

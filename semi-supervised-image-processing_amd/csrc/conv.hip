@@ -108,6 +108,11 @@ struct ConvArgs {
   int xcd_remap;  // 1: XCD-aware workgroup -> tile order (LDS-DMA kernel)
   int dma_mid;  // LDS-DMA ring: the next stage's pieces after the k-step's reads, before its second MFMA half (SSIP_DMA_MID)
   int stagger;  // LDS-DMA ring: waves NW/2.. run each k-step's second MFMA half after the next barrier (SSIP_STAGGER)
+  // INBN (LDS-DMA ring, FWD's A / WGRAD's B operand): the conv input is
+  // relu(fma(y, in_scale[c], in_shift[c])) of the layer below, formed in place
+  // in the ring after each wave's own pieces land (ssip_conv_*_bnrelu_in)
+  const float* in_scale;
+  const float* in_shift;
   // FWD of a 3x3 / stride-s conv fused with its block's 1x1 / stride-s
   // downsample (ssip_conv_fwd_ds): workgroups >= fwd_tiles1 compute the
   // downsample's tiles -- its input pixel is the conv's tap (1, 1) pixel, so
@@ -911,6 +916,29 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_block, 16, voff, 0, 0, 0);
 }
 
+// relu(fma(v, scale, shift)) over the 8 channels c0 .. c0 + 7 of one LDS
+// chunk, in place -- bn_apply_kernel's arithmetic exactly, so a conv over the
+// transformed tile equals the conv of the materialised BN+ReLU output
+__device__ __forceinline__ bf16x8 bnrelu8(bf16x8 v, const float (&sc)[8], const float (&sh)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = __builtin_fmaf((float)v[j], sc[j], sh[j]);
+    t = t > 0.f ? t : 0.f;
+    v[j] = (__bf16)t;
+  }
+  return v;
+}
+__device__ __forceinline__ void bnrelu_chunk(char* p, const float (&sc)[8], const float (&sh)[8]) {
+  bf16x8 v = *reinterpret_cast<bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = __builtin_fmaf((float)v[j], sc[j], sh[j]);
+    t = t > 0.f ? t : 0.f;
+    v[j] = (__bf16)t;
+  }
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
@@ -933,8 +961,12 @@ constexpr int glds_min_waves(int bm, int bn, int nw, int nstage, bool wg) {
 // (Round 3's timing ablations of this k-loop, its 5- and 8-phase ping-pong
 // schedules and the persistent row-balanced halo kernel conv_hb -- all
 // measured no faster in the step -- live on the r3-variants branch.)
+// INBN: FWD / WGRAD over relu(bn(y)) of the layer below (ConvArgs::in_scale),
+// the transform applied to each wave's own landed pieces before the k-step's
+// barrier (2-stage ring; input channels <= GLDS_INBN_C).
+constexpr int GLDS_INBN_C = 512;
 template <int MODE, int BM, int BN, int WMW, int WNW, int NSTAGE, bool C4 = false, bool POST = false,
-          bool FOLD = false>
+          bool FOLD = false, bool INBN = false>
 __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * WNW, NSTAGE, MODE == 2))
     conv_glds_kernel(const ConvArgs a) {
   typedef __bf16 T;
@@ -954,7 +986,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   static_assert(FM >= 1 && FN >= 1, "bad wave tile");
   constexpr int EPI = WG ? 0 : BM * (BN * 2 + 16);
   constexpr int SMEM = (NBUF * STAGE > EPI) ? NBUF * STAGE : EPI;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  static_assert(!INBN || (NSTAGE == 2 && !C4 && !POST && !FOLD && MODE != MODE_DGRAD), "INBN: FWD / WGRAD, 2 stages");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (INBN ? 2 * GLDS_INBN_C * 4 : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1193,9 +1226,15 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
     }
   }
 
+  // INBN: per ring stage, which of this wave's pieces read real input (bit t;
+  // padding taps, rows past the grid and split tails stay zero) and, FWD, the
+  // channel offset of the k-step
+  uint32_t inb_v0 = 0, inb_v1 = 0;
+  int inb_k0 = 0, inb_k1 = 0;
   auto issue = [&](int ks, int stage) {
     char* As = smem + stage * STAGE;
     char* Bs = As + A_BYTES;
+    uint32_t inb_v = 0;
     if constexpr (MODE == MODE_FWD && C4) {
 #pragma unroll
       for (int t = 0; t < LA; ++t) {
@@ -1213,6 +1252,10 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       for (int t = 0; t < LA; ++t) {
         const bool ok = (a_msk[t] >> tp) & 1u;
         blds16(rsA, ok ? a_off[t] + toff : SSIP_OOB, As + (wave + NW * t) * 1024);
+        if constexpr (INBN) inb_v |= (ok ? 1u : 0u) << t;
+      }
+      if constexpr (INBN) {
+        if (stage == 0) { inb_v0 = inb_v; inb_k0 = kcb; } else { inb_v1 = inb_v; inb_k1 = kcb; }
       }
     } else if constexpr (MODE == MODE_DGRAD) {
       if (dsx && ks == a.ds_from) {
@@ -1264,6 +1307,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
         const bool ok = b_row[t] < mlim && (uint32_t)(w_p[t] - w_plo[t]) < (uint32_t)w_pn[t] &&
                         (uint32_t)(w_q[t] - w_qlo[t]) < (uint32_t)w_qn[t];
         blds16(rsB, ok ? w_pix[t] : SSIP_OOB, Bs + (wave + NW * t) * 1024);
+        if constexpr (INBN) inb_v |= (ok ? 1u : 0u) << t;
         // advance the slot's row by the 64 rows of a k-step
         int q = w_q[t] + a.wg_dq;
         const bool c1 = q >= a.Q;
@@ -1274,6 +1318,9 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
         w_q[t] = q;
         w_p[t] = pp;
         w_pix[t] += (uint32_t)(a.wg_k0 + (c1 ? a.wg_e1 : 0) + (c2 ? a.wg_e2 : 0));
+      }
+      if constexpr (INBN) {
+        if (stage == 0) inb_v0 = inb_v; else inb_v1 = inb_v;
       }
     }
     if constexpr (!WG) {
@@ -1303,6 +1350,40 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   // fused-BN epilogue operands: issued first, landed long before the epilogue
   BnPostRegs<T, BM, BN, 64 * WMW * WNW> post;
   if constexpr (MODE == MODE_DGRAD && POST) post.load(a, m0, n0);
+  float* const inb_sc = reinterpret_cast<float*>(smem + SMEM);
+  float* const inb_sh = inb_sc + GLDS_INBN_C;
+  if constexpr (INBN) {
+    for (int c = tid; c < a.C; c += 64 * NW) {
+      inb_sc[c] = a.in_scale[c];
+      inb_sh[c] = a.in_shift[c];
+    }
+    __syncthreads();
+  }
+  // INBN: this wave's landed pieces of `stage` become relu(fma(y, scale, shift))
+  // in place (bn_apply_kernel's arithmetic: fp32 fma, ReLU, one bf16 rounding),
+  // so the k-step's fragment reads see the conv input itself
+  auto inbn_xform = [&](int stage) {
+    if constexpr (INBN) {
+      const uint32_t vb = stage == 0 ? inb_v0 : inb_v1;
+      char* const base = smem + stage * STAGE + (WG ? A_BYTES : 0);
+      constexpr int LP = WG ? LB : LA;
+#pragma unroll
+      for (int t = 0; t < LP; ++t) {
+        if ((vb >> t) & 1u) {
+          int c0;
+          if constexpr (WG) c0 = b_c[t];
+          else c0 = (stage == 0 ? inb_k0 : inb_k1) + a_c[t] * 8;
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(inb_sc + c0);
+          const f32x4 s1 = *reinterpret_cast<const f32x4*>(inb_sc + c0 + 4);
+          const f32x4 h0 = *reinterpret_cast<const f32x4*>(inb_sh + c0);
+          const f32x4 h1 = *reinterpret_cast<const f32x4*>(inb_sh + c0 + 4);
+          const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+          const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+          bnrelu_chunk(base + (wave + NW * t) * 1024 + lane * 16, sc8, sh8);
+        }
+      }
+    }
+  };
   if (nsteps > 0) issue(0, 0);
   if (NSTAGE == 3 && nsteps > 1) issue(1, 1);
   int stage = 0;
@@ -1319,8 +1400,27 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   // results are the same bits.
   const bool lag = a.stagger != 0 && wave >= NW / 2;
   for (int ks = 0; ks < nsteps; ++ks) {
-    if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_barrier<L>(); else wait_vm_barrier<0>();
-    if (lag && ks > 0) {
+    bool deferred = lag && ks > 0;
+    if constexpr (INBN) {
+      // own pieces landed -> transform them -> publish (LDS writes, barrier);
+      // the lagging half's deferred MFMAs (registers only) go first, beside
+      // the leading half's transform
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (deferred) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[1][i], fb[1][j]);
+        deferred = false;
+      }
+      inbn_xform(stage);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (NSTAGE == 3 && ks + 1 < nsteps) {
+      wait_vm_barrier<L>();
+    } else {
+      wait_vm_barrier<0>();
+    }
+    if (deferred) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1707,29 +1807,6 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
 // mask from the BN affine (y is the only extra operand: one load batch per
 // tile); 2 = any other post-op operand set (one load batch per row group:
 // the registers hold no more without spilling)
-// relu(fma(v, scale, shift)) over the 8 channels c0 .. c0 + 7 of one LDS
-// chunk, in place -- bn_apply_kernel's arithmetic exactly, so a conv over the
-// transformed tile equals the conv of the materialised BN+ReLU output
-__device__ __forceinline__ bf16x8 bnrelu8(bf16x8 v, const float (&sc)[8], const float (&sh)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float t = __builtin_fmaf((float)v[j], sc[j], sh[j]);
-    t = t > 0.f ? t : 0.f;
-    v[j] = (__bf16)t;
-  }
-  return v;
-}
-__device__ __forceinline__ void bnrelu_chunk(char* p, const float (&sc)[8], const float (&sh)[8]) {
-  bf16x8 v = *reinterpret_cast<bf16x8*>(p);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float t = __builtin_fmaf((float)v[j], sc[j], sh[j]);
-    t = t > 0.f ? t : 0.f;
-    v[j] = (__bf16)t;
-  }
-  *reinterpret_cast<bf16x8*>(p) = v;
-}
-
 template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool ADD = false, bool INBN = false>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
@@ -3239,8 +3316,30 @@ static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st
   return false;
 }
 
+// the LDS-DMA ring configurations with the BN+ReLU-in operand transform
+#define SSIP_GLDS_INBN_FD(X) X(128, 128, 4, 2, 2) X(128, 64, 4, 2, 2) X(256, 256, 4, 2, 2)
+#define SSIP_GLDS_INBN_WG(X) X(128, 128, 4, 2, 2)
+
 template <int MODE>
 static int launch_glds(const Plan& pl, hipStream_t st) {
+  if constexpr (MODE != MODE_DGRAD) {
+    if (pl.args.in_scale != nullptr) {
+#define SSIP_GLDS_GOI(BM_, BN_, WM_, WN_, ST_)                                                                \
+  if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
+    SSIP_KLAUNCH((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_, false, false, false, true>), pl.grid,      \
+                 dim3(64 * WM_ * WN_), 0, st, pl.args);                                                       \
+    return ::ssip::check_launch("conv_glds_inbn");                                                            \
+  }
+      if constexpr (MODE == MODE_WGRAD) {
+        SSIP_GLDS_INBN_WG(SSIP_GLDS_GOI)
+      } else {
+        SSIP_GLDS_INBN_FD(SSIP_GLDS_GOI)
+      }
+#undef SSIP_GLDS_GOI
+      ::ssip::set_error("no BN+ReLU-in conv kernel for %dx%d/%dx%d/%d", pl.bm, pl.bn, pl.wmw, pl.wnw, pl.stages);
+      return SSIP_ERR_ARG;
+    }
+  }
 #define SSIP_GLDS_GO(BM_, BN_, WM_, WN_, ST_)                                                                 \
   if (pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_) {                   \
     SSIP_KLAUNCH((conv_glds_kernel<MODE, BM_, BN_, WM_, WN_, ST_>), pl.grid, dim3(64 * WM_ * WN_), 0,   \
@@ -3789,6 +3888,42 @@ int64_t ssip_conv_dgrad_bn_partial_floats(const ssip_conv_desc* d) {
   return tiles * d->C * 2 + fin_scratch_floats(d->C, tiles, 2);  // + ssip_bn_bwd_from_partials' split scratch
 }
 
+static int wgrad_implicit(Plan& pl, const ssip_conv_desc* d, int dtype, const void* dy, const void* x,
+                          float* dw_kcrs, int c_real, int s_real, int accumulate, void* workspace, hipStream_t st);
+
+// ssip_conv_*_bnrelu_in beyond the layer-1 halo geometry: the LDS-DMA ring
+// kernels with the INBN operand transform, for bf16 stride-1 convs with
+// 64 <= C <= GLDS_INBN_C input channels -- 1x1 / pad 0 (the ResNet-50
+// bottleneck's conv3 over relu(bn2(y2))) with SSIP_BNRELU_GLDS bit 0, 3x3 /
+// pad 1 with bit 1.  The transform keeps padding taps, rows past the grid
+// and split tails zero.
+static int bnrelu_glds_mask() {
+  const char* e = getenv("SSIP_BNRELU_GLDS");
+  return e != nullptr ? atoi(e) : 0;
+}
+
+static bool glds_inbn_plan(int mode, const ssip_conv_desc* d, int dtype, Plan& pl, int budget = 0) {
+  if (dtype != SSIP_BF16 || !desc_ok(d) || d->stride != 1 || d->C % 64 || d->C > GLDS_INBN_C || d->K % 64)
+    return false;
+  const int m = bnrelu_glds_mask();
+  const bool g1 = d->R == 1 && d->S == 1 && d->pad == 0 && (m & 1);
+  const bool g3 = d->R == 3 && d->S == 3 && d->pad == 1 && (m & 2);
+  if (!g1 && !g3) return false;
+  HaloPlan hp;
+  if (halo_plan(MODE_FWD, d, dtype, hp)) return false;
+  if (plan_conv(mode, d, 2, pl, budget) != SSIP_OK || pl.conv1 || pl.stages != 2) return false;
+  bool ok = false;
+#define SSIP_GLDS_INBN_EQ(BM_, BN_, WM_, WN_, ST_) \
+  ok |= pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_;
+  if (mode == MODE_WGRAD) {
+    SSIP_GLDS_INBN_WG(SSIP_GLDS_INBN_EQ)
+  } else {
+    SSIP_GLDS_INBN_FD(SSIP_GLDS_INBN_EQ)
+  }
+#undef SSIP_GLDS_INBN_EQ
+  return ok;
+}
+
 // the kernel ssip_conv_dgrad_bn runs: the halo kernel where it applies, else
 // the implicit-GEMM kernels at their 128-row tiles (no phase split)
 static int dgrad_bn_plan(const ssip_conv_desc* d, int dtype, Plan& pl, HaloPlan& hp, bool& halo) {
@@ -3910,6 +4045,14 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
       return launch_halo_wgrad(d, hp, dy, x, dw_kcrs, c_real, s_real, accumulate, workspace, workspace_bytes,
                                max_workgroups, (hipStream_t)stream, nullptr, nullptr);
   }
+  return wgrad_implicit(pl, d, dtype, dy, x, dw_kcrs, c_real, s_real, accumulate, workspace, (hipStream_t)stream);
+}
+
+// the split-K implicit-GEMM wgrad of a planned conv + its fixed-order slab
+// reduce (ssip_conv_wgrad_budget; ssip_conv_wgrad_bnrelu_in with in_scale set)
+static int wgrad_implicit(Plan& pl, const ssip_conv_desc* d, int dtype, const void* dy, const void* x,
+                          float* dw_kcrs, int c_real, int s_real, int accumulate, void* workspace, hipStream_t st) {
+  int rc;
   pl.args.A = dy; pl.args.B = x; pl.args.out = workspace;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->P * d->Q * d->K * 2);
   pl.args.b_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
@@ -3924,7 +4067,6 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
     g.wg_e1 = (d->stride * d->W - d->Q * d->stride) * d->C * 2;
     g.wg_e2 = (d->H * d->W - d->P * d->stride * d->W) * d->C * 2;
   }
-  hipStream_t st = (hipStream_t)stream;
   SSIP_DISPATCH_DTYPE(dtype, T, rc = launch_conv<MODE_WGRAD, T>(pl, st));
   if (rc) return rc;
   const int RS = d->R * d->S;
@@ -3990,30 +4132,50 @@ int ssip_stem_bwd_wgrad(const ssip_conv_desc* d, int dtype, const void* dpool, c
 
 int ssip_conv_bnrelu_in_supported(const ssip_conv_desc* d, int dtype) {
   HaloPlan hp, hw;
-  return (halo_plan(MODE_FWD, d, dtype, hp) && halo_wg_plan(d, dtype, hw)) ? 1 : 0;
+  if (halo_plan(MODE_FWD, d, dtype, hp) && halo_wg_plan(d, dtype, hw)) return 1;
+  Plan pf, pw;
+  return (glds_inbn_plan(MODE_FWD, d, dtype, pf) && glds_inbn_plan(MODE_WGRAD, d, dtype, pw)) ? 1 : 0;
 }
 
 int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in, const float* in_scale,
                             const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* z_out,
                             void* stream) {
   HaloPlan hp;
-  SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype) && halo_plan(MODE_FWD, d, dtype, hp), SSIP_ERR_ARG,
-               "ssip_conv_fwd_bnrelu_in: only the layer-1 halo geometry (3x3 / 1 / 1, 64 -> 64, bf16)");
+  SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype), SSIP_ERR_ARG,
+               "ssip_conv_fwd_bnrelu_in: unsupported geometry (ssip_conv_bnrelu_in_supported)");
   SSIP_REQUIRE(y_in && in_scale && in_shift && w_krsc && y, SSIP_ERR_ARG, "ssip_conv_fwd_bnrelu_in: null pointer");
-  return launch_halo(MODE_FWD, d, hp, y_in, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream, nullptr, 0,
-                     nullptr, in_scale, in_shift, z_out);
+  if (halo_plan(MODE_FWD, d, dtype, hp))
+    return launch_halo(MODE_FWD, d, hp, y_in, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream, nullptr, 0,
+                       nullptr, in_scale, in_shift, z_out);
+  Plan pl;
+  SSIP_REQUIRE(z_out == nullptr && glds_inbn_plan(MODE_FWD, d, dtype, pl), SSIP_ERR_ARG,
+               "ssip_conv_fwd_bnrelu_in: z_out only on the layer-1 halo geometry");
+  pl.args.A = y_in; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
+  pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
+  pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);
+  pl.args.in_scale = in_scale; pl.args.in_shift = in_shift;
+  return launch_glds<MODE_FWD>(pl, (hipStream_t)stream);
 }
 
 int ssip_conv_wgrad_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* dy, const void* y_in,
                               const float* in_scale, const float* in_shift, float* dw_kcrs, int accumulate,
                               void* workspace, int64_t workspace_bytes, int max_workgroups, void* stream) {
   HaloPlan hp;
-  SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype) && halo_wg_plan(d, dtype, hp), SSIP_ERR_ARG,
-               "ssip_conv_wgrad_bnrelu_in: only the layer-1 halo geometry (3x3 / 1 / 1, 64 -> 64, bf16)");
+  SSIP_REQUIRE(ssip_conv_bnrelu_in_supported(d, dtype), SSIP_ERR_ARG,
+               "ssip_conv_wgrad_bnrelu_in: unsupported geometry (ssip_conv_bnrelu_in_supported)");
   SSIP_REQUIRE(dy && y_in && in_scale && in_shift && dw_kcrs && workspace && max_workgroups >= 0, SSIP_ERR_ARG,
                "ssip_conv_wgrad_bnrelu_in: bad arguments");
-  return launch_halo_wgrad(d, hp, dy, y_in, dw_kcrs, d->C, d->S, accumulate, workspace, workspace_bytes,
-                           max_workgroups, (hipStream_t)stream, in_scale, in_shift);
+  if (halo_wg_plan(d, dtype, hp))
+    return launch_halo_wgrad(d, hp, dy, y_in, dw_kcrs, d->C, d->S, accumulate, workspace, workspace_bytes,
+                             max_workgroups, (hipStream_t)stream, in_scale, in_shift);
+  Plan pl;
+  SSIP_REQUIRE(glds_inbn_plan(MODE_WGRAD, d, dtype, pl, max_workgroups), SSIP_ERR_ARG,
+               "ssip_conv_wgrad_bnrelu_in: no LDS-DMA BN+ReLU-in plan under this budget");
+  const int64_t need = (int64_t)pl.splits * pl.args.M * pl.args.Ng * 4;
+  SSIP_REQUIRE(workspace_bytes >= need, SSIP_ERR_WORKSPACE, "wgrad workspace too small: %lld < %lld",
+               (long long)workspace_bytes, (long long)need);
+  pl.args.in_scale = in_scale; pl.args.in_shift = in_shift;
+  return wgrad_implicit(pl, d, dtype, dy, y_in, dw_kcrs, d->C, d->S, accumulate, workspace, (hipStream_t)stream);
 }
 
 /* Which kernel a conv pass selects for this geometry (tests / tuning): writes a

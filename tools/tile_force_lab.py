@@ -25,13 +25,23 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--r50", action="store_true", help="ResNet-50 1x1 shapes at 512^2 (BASELINE config 5)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     bf = torch.bfloat16
     torch.manual_seed(0)
     part = torch.empty(16 << 20, device=dev)
     want = a.shapes.split(",")
-    for nm, g in shapes(a.batch):
+    if a.r50:
+        # name, H, C, K (1x1, stride 1) at 512^2: layer1 128^2, layer2 64^2, layer3 32^2, layer4 16^2
+        r50 = [("l1.conv1a", 128, 64, 64), ("l1.conv1", 128, 256, 64), ("l1.conv3", 128, 64, 256),
+               ("l2.conv1", 64, 512, 128), ("l2.conv3", 64, 128, 512), ("l3.conv1", 32, 1024, 256),
+               ("l3.conv3", 32, 256, 1024), ("l4.conv1", 16, 2048, 512), ("l4.conv3", 16, 512, 2048)]
+        shape_list = [(nm, ops.ConvGeom(a.batch, H, H, C, K, 1, 1, 1, 0, C, 1)) for nm, H, C, K in r50]
+        want = [nm for nm, _ in shape_list]
+    else:
+        shape_list = shapes(a.batch)
+    for nm, g in shape_list:
         if nm not in want:
             continue
         x = torch.randn(g.N, g.H, g.W, g.C, device=dev).to(bf)

@@ -3089,7 +3089,9 @@ static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st);
 static int device_cus();
 // SSIP_WGRAD_BIG: 1 = the budget's 16-wave 256-column tiles for every 3x3
-// wgrad, 2 = only the 256x256 ones (K % 256 == 0); unset / 0 = the full-grid
+// wgrad, 2 = only the 256x256 ones (K % 256 == 0), 3 = 8-wave 256x256 tiles
+// for those, 4 = those and 8-wave 128x256 tiles for K = 128 (round 6, with
+// the stagger; both on SSIP_WGRAD_BIG_CUS percent of the CUs); unset / 0 = the full-grid
 // tiles (default: faster alone, but the step measured 6.34 vs 6.19 ms with
 // them -- a 16-wave workgroup holding every register of its CU keeps the main
 // stream's dgrad / BN chain off it; profiles/r5_wgrad_lab.txt, r5_ab.txt)
@@ -3221,9 +3223,20 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   if (mode == MODE_WGRAD && wg_budget > 0 && pl.stages > 0 && !pl.conv1 && bigm > 0) {
     // (the 1x1 downsample wgrads, Ng <= 256, keep their many-tile grids)
     if (a.M % 256 == 0 && a.Ng % 256 == 0 && a.Ng >= 512) {
-      pl.bm = 256; pl.bn = 256; pl.wmw = 4; pl.wnw = 4;
+      // 3, 4: the 8-wave 256x256 tile (with the stagger: l3 / l4 3x3 wgrads
+      // at the budget 98 -> 73 us, profiles/r6_tile_lab.txt)
+      pl.bm = 256; pl.bn = 256; pl.wmw = 4; pl.wnw = bigm >= 3 ? 2 : 4;
     } else if (bigm == 1 && a.M % 128 == 0 && a.Ng >= 512) {
       pl.bm = 128; pl.bn = 256; pl.wmw = 4; pl.wnw = 4;  // a partial last tile where Ng % 256 != 0
+    } else if (bigm == 4 && a.M % 128 == 0 && a.Ng >= 512) {
+      pl.bm = 128; pl.bn = 256; pl.wmw = 2; pl.wnw = 4;  // 8 waves, 96 KiB of LDS
+    }
+    if (bigm >= 3 && pl.bn == 256) {
+      // on SSIP_WGRAD_BIG_CUS percent of the budget's CUs, the rest left to the
+      // main stream (measured: profiles/r6_tile_lab.txt)
+      const char* e = getenv("SSIP_WGRAD_BIG_CUS");
+      const int pc = e ? std::max(1, std::min(100, atoi(e))) : 100;
+      wg_budget = std::max(1, wg_budget * pc / 100);
     }
   }
   if (int rc = apply_force(mode, elem_bytes, pl)) return rc;

@@ -54,6 +54,7 @@ for r in rows:
                                                                           int(r["End_Timestamp"]))})
     d[r["Counter_Name"]] = float(r["Counter_Value"])
 ds = list(disp.values())
+HAVE_COEXEC = any("SQ_VALU_MFMA_COEXEC_CYCLES" in d for d in ds)
 idx = [i for i, d in enumerate(ds) if "weight_prep_batch" in d["name"] and
        (i == 0 or "weight_prep_batch" not in ds[i - 1]["name"])]  # the step head (1-2 launches)
 step = ds[idx[-2] + 1: idx[-1] + 1]
@@ -66,16 +67,18 @@ for d in step:
         tgt["dur"] += dur
         tgt["gui"] += d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS
         for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
-                  "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES"):
+                  "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES", "SQ_VALU_MFMA_COEXEC_CYCLES"):
             tgt[c] += d.get(c, 0.0)
 
 lines = ["# MFMA busy per kernel, one step of `bench.py` (rocprofv3 --pmc, profiled clocks run lower than",
          f"# unprofiled: MI355X_MICROARCH.md DVFS item 2).  mfma = MFMA_BUSY / (trace duration * {SCLK_MHZ:.0f} MHz"
          " * 1024 SIMDs);",
          "# gui_mfma = MFMA_BUSY / (GUI_ACTIVE/8 * 1024 SIMDs) (round 4's normalisation; guiGHz = GUI_ACTIVE/8 / us);",
-         "# wait/inst = SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY as fractions of SQ_WAVE_CYCLES",
+         "# wait/inst = SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY as fractions of SQ_WAVE_CYCLES;",
+         "# coexec = SQ_VALU_MFMA_COEXEC_CYCLES (vector and matrix instructions executing together) normalised as mfma",
+         "# (blank when the pass did not collect it)",
          f"{'kernel':82s} {'n':>3s} {'us':>8s} {'mfma':>6s} {'guiGHz':>6s} {'gui_mfma':>8s} {'wait':>5s} {'winst':>5s}"
-         f" {'active':>6s}"]
+         f" {'active':>6s} {'coexec':>6s}"]
 
 
 def fmt(k, v):
@@ -83,8 +86,10 @@ def fmt(k, v):
     util = v["SQ_VALU_MFMA_BUSY_CYCLES"] / max(v["dur"] * SCLK_MHZ * 1e6 * CUS * SIMDS, 1.0)
     gutil = v["SQ_VALU_MFMA_BUSY_CYCLES"] / max(v["gui"] * CUS * SIMDS, 1.0)
     ghz = v["gui"] / max(v["dur"], 1e-12) / 1e9
+    co = v["SQ_VALU_MFMA_COEXEC_CYCLES"] / max(v["dur"] * SCLK_MHZ * 1e6 * CUS * SIMDS, 1.0)
+    cos = f"{co:6.1%}" if HAVE_COEXEC else ""
     return (f"{k:82s} {int(v['n']):3d} {v['dur'] * 1e6:8.1f} {util:6.1%} {ghz:6.2f} {gutil:8.1%} "
-            f"{v['SQ_WAIT_ANY'] / wc:5.2f} {v['SQ_WAIT_INST_ANY'] / wc:5.2f} {v['SQ_ACTIVE_INST_ANY'] / wc:6.2f}")
+            f"{v['SQ_WAIT_ANY'] / wc:5.2f} {v['SQ_WAIT_INST_ANY'] / wc:5.2f} {v['SQ_ACTIVE_INST_ANY'] / wc:6.2f} {cos}")
 
 
 for k, v in sorted(agg.items(), key=lambda kv: -kv[1]["dur"]):

@@ -943,6 +943,14 @@ template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// the same with every LDS read of this wave retired first: with the stagger a
+// lagging wave's second-half fragments are read before the barrier but used
+// after it, and nothing else keeps those reads ahead of the next refill of
+// their ring slot, which other waves issue right after the barrier
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 
 // Waves per SIMD the LDS budget allows; asking the compiler for that many
 // keeps the register count from costing a resident workgroup.
@@ -1415,6 +1423,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
       }
       inbn_xform(stage);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (a.stagger) {
+      if (NSTAGE == 3 && ks + 1 < nsteps) wait_vm_lgkm_barrier<L>(); else wait_vm_lgkm_barrier<0>();
     } else if (NSTAGE == 3 && ks + 1 < nsteps) {
       wait_vm_barrier<L>();
     } else {
@@ -3088,16 +3098,21 @@ static void pick_tile(int M, int Ng, int elem_bytes, Plan& pl) {
 
 static bool glds_has(int mode, bool stem, int bm, int bn, int wm, int wn, int st);
 static int device_cus();
-// SSIP_WGRAD_BIG: 1 = the budget's 16-wave 256-column tiles for every 3x3
-// wgrad, 2 = only the 256x256 ones (K % 256 == 0), 3 = 8-wave 256x256 tiles
-// for those, 4 = those and 8-wave 128x256 tiles for K = 128 (round 6, with
-// the stagger; both on SSIP_WGRAD_BIG_CUS percent of the CUs); unset / 0 = the full-grid
-// tiles (default: faster alone, but the step measured 6.34 vs 6.19 ms with
-// them -- a 16-wave workgroup holding every register of its CU keeps the main
-// stream's dgrad / BN chain off it; profiles/r5_wgrad_lab.txt, r5_ab.txt)
+// SSIP_WGRAD_BIG (a wgrad with a budget, i.e. on the side stream): 0 = the
+// full-grid tiles; 1 = 16-wave 256-column tiles for every 3x3 wgrad, 2 = only
+// the 256x256 ones (K % 256 == 0) -- round 5: faster alone, slower in the step
+// (6.34 vs 6.19 ms), a 16-wave workgroup holding every register of its CU
+// keeps the main stream's dgrad / BN chain off it; 3 = 8-wave 256x256 tiles
+// for those; 4 (default) = those and 8-wave 128x256 tiles where 128 <= K <
+// 256, both on SSIP_WGRAD_BIG_CUS (default 62) percent of the budget's CUs,
+// the rest of the chip left to the main stream.  Round 6, with the stagger
+// (tools/gpu_r6_{i,j,k}.sh, alternated runs on one box each, ms/step): mode 4
+// on 62 % of the CUs 5.937 vs 6.013 (4 + 4; 56 % 5.969, 70 % 5.979, 80 %
+// 6.083), 5.933 vs 6.018 on another box; mode 3 at 62 % 5.985; mode 3 on
+// every CU 5.98 vs 5.87 (profiles/r6_wgrad_big_ab.txt)
 static int wgrad_big_mode() {
   const char* e = getenv("SSIP_WGRAD_BIG");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 4;
 }
 
 // Default LDS-DMA configuration for a bf16 GEMM view (M x Ng, reduction Kg).
@@ -3235,7 +3250,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
       // on SSIP_WGRAD_BIG_CUS percent of the budget's CUs, the rest left to the
       // main stream (measured: profiles/r6_tile_lab.txt)
       const char* e = getenv("SSIP_WGRAD_BIG_CUS");
-      const int pc = e ? std::max(1, std::min(100, atoi(e))) : 100;
+      const int pc = e ? std::max(1, std::min(100, atoi(e))) : 62;
       wg_budget = std::max(1, wg_budget * pc / 100);
     }
   }

@@ -27,18 +27,19 @@ N = 256
 CONVS = [
     ("l1.3x3", (64, 56, 64, 3, 1, 1), {"fwd": "halo<fwd", "dgrad": "halo<dgrad", "wgrad": "halo_wgrad<"}),
     ("l2.0.conv1", (64, 56, 128, 3, 2, 1), {"fwd": "glds<fwd,128x128", "dgrad": "glds<dgrad,128x64,4x2,2,phased",
-                                            "wgrad": "glds<wgrad,128x128"}),
+                                            "wgrad": "glds<wgrad,128x128", "budget": "glds<wgrad,128x256,2x4,2"}),
     ("l2.3x3", (128, 28, 128, 3, 1, 1), {"fwd": "glds<fwd,128x128", "dgrad": "glds<dgrad,128x128",
-                                         "wgrad": "glds<wgrad,128x128"}),
+                                         "wgrad": "glds<wgrad,128x128", "budget": "glds<wgrad,128x256,2x4,2"}),
     ("l2.ds", (64, 56, 128, 1, 2, 0), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad"}),
     ("l3.0.conv1", (128, 28, 256, 3, 2, 1), {"fwd": "glds<fwd", "dgrad": "glds<dgrad,128x128,4x2,2,phased",
-                                             "wgrad": "glds<wgrad"}),
+                                             "wgrad": "glds<wgrad", "budget": "glds<wgrad,128x256,2x4,2"}),
     ("l3.3x3", (256, 14, 256, 3, 1, 1), {"fwd": "glds<fwd,256x256,4x2,2", "dgrad": "glds<dgrad,256x256,4x2,2",
-                                         "wgrad": "glds<wgrad,128x128"}),
+                                         "wgrad": "glds<wgrad,128x128", "budget": "glds<wgrad,256x256,4x2,2"}),
     ("l3.ds", (128, 28, 256, 1, 2, 0), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad"}),
     ("l4.0.conv1", (256, 14, 512, 3, 2, 1), {"fwd": "glds<fwd", "dgrad": "glds<dgrad,128x128,4x2,2,phased",
-                                             "wgrad": "glds<wgrad"}),
-    ("l4.3x3", (512, 7, 512, 3, 1, 1), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad"}),
+                                             "wgrad": "glds<wgrad", "budget": "glds<wgrad,256x256,4x2,2"}),
+    ("l4.3x3", (512, 7, 512, 3, 1, 1), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad",
+                                        "budget": "glds<wgrad,256x256,4x2,2"}),
     ("l4.ds", (256, 14, 512, 1, 2, 0), {"fwd": "glds<fwd", "dgrad": "glds<dgrad", "wgrad": "glds<wgrad"}),
 ]
 DT = torch.bfloat16
@@ -145,7 +146,7 @@ def test_wgrad_bs256(dev, name, shape, kern):
     from ssip.resnet import _side_wgrad_budget
 
     budgets = (_side_wgrad_budget(g, DT, dev), 7)
-    if "budget" in kern:  # the side stream's production kernel (ABI 12: 16-wave wide tiles)
+    if "budget" in kern:  # the side stream's production kernel (round 6: 8-wave wide tiles on 62 % of the CUs)
         assert ops.conv_kernel_name("wgrad", g, DT, budgets[0]).startswith(kern["budget"]), \
             ops.conv_kernel_name("wgrad", g, DT, budgets[0])
     dwb = []

@@ -3184,7 +3184,8 @@ static int stagger_for(int mode, const Plan& pl) {
   return (m >> mode) & 1;
 }
 
-static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl, int wg_budget = 0) {
+static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl, int wg_budget = 0,
+                     bool allow_big = true) {
   SSIP_REQUIRE(desc_ok(d), SSIP_ERR_ARG, "bad conv descriptor");
   pl.mode = mode;
   pl.conv1 = (d->C == 4);
@@ -3231,7 +3232,7 @@ static int plan_conv(int mode, const ssip_conv_desc* d, int elem_bytes, Plan& pl
   // (tools/wgrad_lab.py at the 256-workgroup budget, profiles/r5_wgrad_lab.txt:
   // l2.3x3 110.9 -> 89.1 us with 128x256, l3.3x3 109.9 -> 73.9 and l4.3x3
   // 101.4 -> 75.4 with 256x256) -- but not in the step (wgrad_big_mode)
-  const int bigm = mode == MODE_WGRAD ? wgrad_big_mode() : 0;
+  const int bigm = (mode == MODE_WGRAD && allow_big) ? wgrad_big_mode() : 0;
   // (round 5 also measured 8-wave 128x256 tiles at the budget -- two waves
   // per SIMD, 96 KiB of LDS, so not the whole CU: 517.6 -> 461.1 us over the
   // six layer 2-4 wgrads, but the step 6.14 -> 6.43 ms, 4 + 4 runs)
@@ -3939,7 +3940,8 @@ static bool glds_inbn_plan(int mode, const ssip_conv_desc* d, int dtype, Plan& p
   if (!g1 && !g3) return false;
   HaloPlan hp;
   if (halo_plan(MODE_FWD, d, dtype, hp)) return false;
-  if (plan_conv(mode, d, 2, pl, budget) != SSIP_OK || pl.conv1 || pl.stages != 2) return false;
+  // (the wide budget tiles of SSIP_WGRAD_BIG have no INBN form: the budget's plain tiles)
+  if (plan_conv(mode, d, 2, pl, budget, false) != SSIP_OK || pl.conv1 || pl.stages != 2) return false;
   bool ok = false;
 #define SSIP_GLDS_INBN_EQ(BM_, BN_, WM_, WN_, ST_) \
   ok |= pl.bm == BM_ && pl.bn == BN_ && pl.wmw == WM_ && pl.wnw == WN_ && pl.stages == ST_;
@@ -4015,6 +4017,8 @@ int64_t ssip_conv_wgrad_workspace_bytes_budget(const ssip_conv_desc* d, int max_
   int64_t b = -1;
   if (max_workgroups < 0) return -1;
   if (plan_conv(MODE_WGRAD, d, 2, p2, max_workgroups) == SSIP_OK) b = (int64_t)p2.splits * p2.args.M * p2.args.Ng * 4;
+  if (max_workgroups > 0 && plan_conv(MODE_WGRAD, d, 2, p2, max_workgroups, false) == SSIP_OK)  // the INBN form's plan
+    b = std::max<int64_t>(b, (int64_t)p2.splits * p2.args.M * p2.args.Ng * 4);
   if (plan_conv(MODE_WGRAD, d, 4, p4, max_workgroups) == SSIP_OK)
     b = std::max<int64_t>(b, (int64_t)p4.splits * p4.args.M * p4.args.Ng * 4);
   HaloPlan hp;

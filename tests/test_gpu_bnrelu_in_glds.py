@@ -42,6 +42,9 @@ CASES = [
 @pytest.mark.parametrize("name,N,H,C,K,R,env", CASES, ids=[c[0] for c in CASES])
 def test_glds_bnrelu_in_matches_apply_then_conv_and_torch(dev, monkeypatch, name, N, H, C, K, R, env):
     monkeypatch.setenv("SSIP_BNRELU_GLDS", env)
+    # the plain wgrad on the budget's plain tiles, as the INBN form plans (the
+    # wide SSIP_WGRAD_BIG tiles have no INBN form): the same splits, same bits
+    monkeypatch.setenv("SSIP_WGRAD_BIG", "0")
     pd = (R - 1) // 2
     g = ConvGeom(N, H, H, C, K, R, R, 1, pd, C, R)
     assert ops.conv_bnrelu_in_supported(g, DT), name

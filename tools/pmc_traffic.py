@@ -27,14 +27,27 @@ def family(n):
     return "other"
 
 
+def short(n):
+    import re
+    n = n.replace("(anonymous namespace)::", "")
+    n = re.sub(r"^void ", "", n)
+    return re.sub(r"\((?![^<]*>).*", "", n)[:70]
+
+
+KERN = {}
+
+
 def per_step(path, counter):
     rows = [r for r in csv.DictReader(open(path)) if r.get("Counter_Name", counter) == counter]
     idx = [i for i, r in enumerate(rows) if "weight_prep_batch" in r["Kernel_Name"] and
            (i == 0 or "weight_prep_batch" not in rows[i - 1]["Kernel_Name"])]  # the step head (1-2 launches)
     a, b = idx[-2], idx[-1]
     fam = collections.Counter()
+    kern = KERN.setdefault(counter, collections.Counter())
     for r in rows[a + 1:b + 1]:
-        fam[family(r["Kernel_Name"])] += float(r["Counter_Value"]) * 1024.0
+        v = float(r["Counter_Value"]) * 1024.0
+        fam[family(r["Kernel_Name"])] += v
+        kern[short(r["Kernel_Name"])] += v
     return fam
 
 
@@ -46,6 +59,17 @@ for k in sorted(set(fetch) | set(write)):
     wr = write.get(k, 0.0)
     out[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr}
     print(f"{k:12s} read {rd / 1e9:8.3f} GB  write {wr / 1e9:8.3f} GB  total {(rd + wr) / 1e9:8.3f} GB per step")
+# per-kernel bytes of the BN family (the per-pass breakdown VERDICT r5 item 3 asks for)
+bnk = {}
+for k in sorted(set(KERN.get("FETCH_SIZE", {})) | set(KERN.get("WRITE_SIZE", {}))):
+    if family(k) != "bn":
+        continue
+    rd = 2.0 * KERN["FETCH_SIZE"].get(k, 0.0)
+    wr = KERN["WRITE_SIZE"].get(k, 0.0)
+    bnk[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr}
+for k, v in sorted(bnk.items(), key=lambda kv: -kv[1]["total_bytes"]):
+    print(f"  bn pass {k:70s} {v['total_bytes'] / 1e9:8.3f} GB")
+out["bn_kernels"] = bnk
 if len(sys.argv) > 4:
     out["_workload"] = sys.argv[4]
 if len(sys.argv) > 3:

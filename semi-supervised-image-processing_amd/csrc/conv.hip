@@ -27,6 +27,8 @@
 // reduction into fp32 slabs that a second kernel sums in fixed order
 // (bitwise reproducible, no atomics).
 #include <algorithm>
+#include <cstdio>
+#include <vector>
 #include "ssip_common.h"
 #include "fin_split.h"
 
@@ -1722,6 +1724,8 @@ struct HaloArgs {
   // in_shift)) is formed in LDS (ssip_conv_fwd_bnrelu_in)
   const float *in_scale, *in_shift;
   __bf16* zout;  // INBN (nullable): the transformed input's own tile rows written out (the wgrad's x)
+  unsigned long long* stamps;  // STAMP instances only (SSIP_HALO_DIAG 128): per wave and tile 3 s_memtime stamps;
+                               // with it, 1 = no output stores, 2 = no MFMAs (compile-time forms, results wrong)
   int diag;  // timing ablations only (SSIP_HALO_DIAG, results wrong): 4 no input-row DMA after the
              // first tile, 8 no BN statistics (round 5's 1 = no stores / 2 = no MFMAs: r5_halo_lab.txt);
              // 16 (results right): the next tile's rows issued before the MFMAs, not among them;
@@ -1742,6 +1746,16 @@ __device__ __forceinline__ int xtile_off(int px, int slot) { return px * 128 + (
 // LDS-only workgroup barrier: __syncthreads() would also drain vmcnt, i.e.
 // wait for the next tile's rows in flight and this tile's output stores
 __device__ __forceinline__ void halo_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }  // one input-row buffer: (TR + 2) * (W + 2) <= 352 pixels
+
+// diagnostic phase stamp (conv_halo_kernel<..., STAMP>): one asm statement with
+// its own lgkmcnt(0) (s_memtime returns out of order with LDS reads), fenced
+__device__ __forceinline__ unsigned long long halo_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 // conv_halo_kernel's DGRAD epilogue with the BN-backward reduction of the
 // BN+ReLU below fused in (ssip_conv_dgrad_bn): per row-fragment i, the
@@ -1817,7 +1831,7 @@ __device__ __forceinline__ void halo_bnpost_epilogue(const HaloArgs& a, const f3
 // mask from the BN affine (y is the only extra operand: one load batch per
 // tile); 2 = any other post-op operand set (one load batch per row group:
 // the registers hold no more without spilling)
-template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool ADD = false, bool INBN = false>
+template <int WMW, int WNW, bool FOLD = false, int BNPOST = 0, bool ADD = false, bool INBN = false, int STAMP = 0>
 __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_kernel(const HaloArgs a) {
   typedef __bf16 T;
   constexpr int NW = WMW * WNW, NT = 64 * NW;
@@ -2016,7 +2030,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
         float t = FOLD ? ac[i][jj][e] + bcol : ac[i][jj][e];
         if (has_add) t = to_f32(from_f32<T>(t)) + to_f32(__builtin_bit_cast(T, ra[i][jj][e]));
         const T o = from_f32<T>(FOLD ? fmaxf(t, lo) : t);
-        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off, 0, 0);
+        if constexpr (!(STAMP & 4)) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, o), rsO, off, 0, 0);
       }
     }
   };
@@ -2070,6 +2084,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     }
     first = false;
     halo_lds_barrier();
+    unsigned long long st0 = 0, st1 = 0;
+    if constexpr (STAMP) st0 = halo_stamp();
     const int un = u + 1;
     const bool more = un < u1;
     const int jn_next = more ? un / a.tiles : jn;
@@ -2133,7 +2149,8 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
+        for (int jj = 0; jj < FN; ++jj)
+          if constexpr (!(STAMP & 2)) mma(acc[i][jj], fa[st & 1][i], fb[st & 1][jj]);
       if (st % 2 == 0 && st / 2 < XPW) {
         const int i = wave + (st / 2) * NW;
         if constexpr (INBN) {
@@ -2161,6 +2178,7 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
     // the next tile's rows (issued before the MFMAs) and this wave's older
     // stores retire here; nothing younger is in flight
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (STAMP) st1 = halo_stamp();
     if constexpr (INBN) {
       // pieces staged too late for the k-loop's stores (XPW + XLAG > 9)
 #pragma unroll
@@ -2203,6 +2221,15 @@ __global__ void __launch_bounds__(64 * WMW * WNW, (WMW * WNW) / 4) conv_halo_ker
 #pragma unroll
       for (int i = 0; i < FM; ++i) epi_rows(acc, i, tile, jn, rap);
       if (stats && !prefetch) stats_flush(jn);
+    }
+    if constexpr (STAMP) {
+      const unsigned long long st2 = halo_stamp();
+      if (lane == 0 && u - u0 < 32) {
+        unsigned long long* sp = a.stamps + (((long)g * NW + wave) * 32 + (u - u0)) * 3;
+        sp[0] = st0;
+        sp[1] = st1;
+        sp[2] = st2;
+      }
     }
     if (more && !prefetch) {
       // panel change: new weights and the next tile's rows, loaded once every
@@ -3704,7 +3731,34 @@ static int launch_halo(int mode, const ssip_conv_desc* d, const HaloPlan& hp, co
     SSIP_KLAUNCH((conv_halo_kernel<4, 2, true>), dim3(hp.G), dim3(512), 0, st, h);
   else if (add != nullptr)
     SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, true>), dim3(hp.G), dim3(512), 0, st, h);
-  else
+  else if (h.diag & 128) {
+    // phase stamps (lab only): per workgroup, wave and tile {after the tile's
+    // barrier, after the k-loop's vmcnt(0), after the epilogue}, written to
+    // SSIP_HALO_STAMP_OUT as raw u64 [G][8][32][3]
+    static unsigned long long* buf = nullptr;
+    const size_t n = (size_t)hp.G * 8 * 32 * 3;
+    if (buf == nullptr && hipMalloc(&buf, n * 8) != hipSuccess) return SSIP_ERR_LAUNCH;
+    (void)hipMemsetAsync(buf, 0, n * 8, st);
+    h.stamps = buf;
+    // compile-time ablations (timing only, results wrong): diag 2 no MFMAs, diag 1 no output stores
+    if ((h.diag & 3) == 3)
+      SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, false, false, 7>), dim3(hp.G), dim3(512), 0, st, h);
+    else if (h.diag & 2)
+      SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, false, false, 3>), dim3(hp.G), dim3(512), 0, st, h);
+    else if (h.diag & 1)
+      SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, false, false, 5>), dim3(hp.G), dim3(512), 0, st, h);
+    else
+      SSIP_KLAUNCH((conv_halo_kernel<4, 2, false, 0, false, false, 1>), dim3(hp.G), dim3(512), 0, st, h);
+    std::vector<unsigned long long> host(n);
+    if (hipMemcpyAsync(host.data(), buf, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return SSIP_ERR_LAUNCH;
+    const char* path = getenv("SSIP_HALO_STAMP_OUT");
+    if (FILE* f = fopen(path ? path : "/tmp/halo_stamps.bin", "wb")) {
+      fwrite(host.data(), 8, n, f);
+      fclose(f);
+    }
+  } else
     SSIP_KLAUNCH((conv_halo_kernel<4, 2>), dim3(hp.G), dim3(512), 0, st, h);
   return ::ssip::check_launch("conv_halo");
 }

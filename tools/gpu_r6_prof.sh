@@ -11,13 +11,15 @@ out=gpurun_out/$tag
 mkdir -p $out
 timeout -k 10 300 python bench.py --no-cpu-baseline "${extra[@]}" > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
 tail -1 $out/bench.log | cut -c1-300
+# the step's conv-family TFLOP from the line itself (R18 3.1895, R50 512^2 18.975)
+tf=$(python3 -c "import json; print(json.loads(open('$out/bench.log').read().strip().splitlines()[-1])['config']['gflop_per_step_per_gpu'] / 1000)")
 for leg in full production; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out/leg_$leg -o run -- \
     python bench.py --profile-leg $leg --steps 3 --warmup 3 --sclk-out $out/sclk_$leg.json "${extra[@]}" \
     > $out/leg_$leg.log 2>&1 || { tail -20 $out/leg_$leg.log; exit 1; }
   f=$(find $out/leg_$leg -name "*kernel_trace.csv" | head -1)
   mhz=$(python3 -c "import json; print(json.load(open('$out/sclk_$leg.json'))['sclk']['mean_mhz'])")
-  python3 tools/roofline_from_trace.py $f --label "leg $leg (SCLK $mhz MHz)" --out $out/roofline_leg_$leg.txt | head -3
+  python3 tools/roofline_from_trace.py $f --tflop $tf --label "leg $leg (SCLK $mhz MHz)" --out $out/roofline_leg_$leg.txt | head -3
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
     SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE --output-format csv \
     -d $out/mfma_$leg -o run -- \
@@ -34,7 +36,7 @@ SSIP_STAGGER=0 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-forma
   > $out/leg_production_s0.log 2>&1 || { tail -20 $out/leg_production_s0.log; exit 1; }
 f=$(find $out/leg_production_s0 -name "*kernel_trace.csv" | head -1)
 mhz=$(python3 -c "import json; print(json.load(open('$out/sclk_production_s0.json'))['sclk']['mean_mhz'])")
-python3 tools/roofline_from_trace.py $f --label "leg production, SSIP_STAGGER=0 (SCLK $mhz MHz)" \
+python3 tools/roofline_from_trace.py $f --tflop $tf --label "leg production, SSIP_STAGGER=0 (SCLK $mhz MHz)" \
   --out $out/roofline_leg_production_s0.txt | head -3
 SSIP_STAGGER=0 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
   SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE --output-format csv \

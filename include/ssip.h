@@ -164,12 +164,12 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
  * another stream.
  * ABI 14: also bf16 stride-1 convs on the LDS-DMA ring kernels with 64 <= C
  * <= 512 input channels -- 1x1 / pad 0 (the ResNet-50 Bottleneck's conv3 over
- * relu(bn2(y2)), $SSIP_BNRELU_GLDS bit 0) and 3x3 / pad 1 (bit 1); both off
- * by default (measured neutral / slower in the steps):
- * each wave transforms the input pieces it DMA'd
- * once they land, before the k-step's barrier; padding taps and rows past
- * the grid stay zero.  Same bits as ssip_bn_apply + the plain conv.  z_out
- * must be NULL there. */
+ * relu(bn2(y2)), $SSIP_BNRELU_GLDS bit 0, on by default) and 3x3 / pad 1
+ * (bit 1, off: slower in the steps): each wave transforms
+ * the input pieces it DMA'd once they land, before the k-step's barrier;
+ * padding taps and rows past the grid stay zero.  Same bits as ssip_bn_apply
+ * + the plain conv.  z_out: also for the 1x1 form (the n-tile-0 workgroups
+ * store each transformed piece), NULL for the 3x3 form. */
 int ssip_conv_bnrelu_in_supported(const ssip_conv_desc* d, int dtype);
 int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in, const float* in_scale,
                             const float* in_shift, const void* w_krsc, void* y, float* bn_partial, void* z_out,

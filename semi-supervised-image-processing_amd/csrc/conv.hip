@@ -115,6 +115,10 @@ struct ConvArgs {
   // in the ring after each wave's own pieces land (ssip_conv_*_bnrelu_in)
   const float* in_scale;
   const float* in_shift;
+  // INBN FWD of a 1x1 / stride-1 conv (nullable): the n-tile-0 workgroups
+  // also store each transformed piece to zout (same layout as A), so the
+  // weight gradient takes relu(bn(y)) as a plain input
+  void* zout;
   // FWD of a 3x3 / stride-s conv fused with its block's 1x1 / stride-s
   // downsample (ssip_conv_fwd_ds): workgroups >= fwd_tiles1 compute the
   // downsample's tiles -- its input pixel is the conv's tap (1, 1) pixel, so
@@ -1362,6 +1366,11 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
   if constexpr (MODE == MODE_DGRAD && POST) post.load(a, m0, n0);
   float* const inb_sc = reinterpret_cast<float*>(smem + SMEM);
   float* const inb_sh = inb_sc + GLDS_INBN_C;
+  // INBN FWD z_out (1x1 / stride 1: a piece's byte offset at tap 0 + the
+  // k-step's channel offset is its input offset, so z has A's layout); only
+  // the n-tile-0 workgroups store (every n-tile reads the same pieces)
+  const bool zst = INBN && MODE == MODE_FWD && a.zout != nullptr && tn == 0;
+  const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(zst ? a.zout : nullptr, zst ? a.a_bytes : 0);
   if constexpr (INBN) {
     for (int c = tid; c < a.C; c += 64 * NW) {
       inb_sc[c] = a.in_scale[c];
@@ -1390,6 +1399,14 @@ __global__ void __launch_bounds__(64 * WMW * WNW, glds_min_waves(BM, BN, WMW * W
           const float sc8[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
           const float sh8[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
           bnrelu_chunk(base + (wave + NW * t) * 1024 + lane * 16, sc8, sh8);
+          if constexpr (!WG) {
+            if (zst) {
+              typedef __attribute__((ext_vector_type(4))) unsigned int zv4u;
+              const zv4u v = *reinterpret_cast<const zv4u*>(base + (wave + NW * t) * 1024 + lane * 16);
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  v, rsZ, a_off[t] + (uint32_t)((stage == 0 ? inb_k0 : inb_k1) * 2), 0, 0);
+            }
+          }
         }
       }
     }
@@ -3980,9 +3997,12 @@ static int wgrad_implicit(Plan& pl, const ssip_conv_desc* d, int dtype, const vo
 // bottleneck's conv3 over relu(bn2(y2))) with SSIP_BNRELU_GLDS bit 0, 3x3 /
 // pad 1 with bit 1.  The transform keeps padding taps, rows past the grid
 // and split tails zero.
+// SSIP_BNRELU_GLDS: bit 0 the 1x1 / stride-1 form (default on: config 5,
+// 60.23 vs 60.60 ms/step with the forward's z_out, profiles/r6_bnrelu_in_glds_lab.txt),
+// bit 1 the 3x3 form (off: slower in both steps)
 static int bnrelu_glds_mask() {
   const char* e = getenv("SSIP_BNRELU_GLDS");
-  return e != nullptr ? atoi(e) : 0;
+  return e != nullptr ? atoi(e) : 1;
 }
 
 static bool glds_inbn_plan(int mode, const ssip_conv_desc* d, int dtype, Plan& pl, int budget = 0) {
@@ -4234,8 +4254,11 @@ int ssip_conv_fwd_bnrelu_in(const ssip_conv_desc* d, int dtype, const void* y_in
     return launch_halo(MODE_FWD, d, hp, y_in, w_krsc, y, nullptr, bn_partial, (hipStream_t)stream, nullptr, 0,
                        nullptr, in_scale, in_shift, z_out);
   Plan pl;
-  SSIP_REQUIRE(z_out == nullptr && glds_inbn_plan(MODE_FWD, d, dtype, pl), SSIP_ERR_ARG,
-               "ssip_conv_fwd_bnrelu_in: z_out only on the layer-1 halo geometry");
+  SSIP_REQUIRE(glds_inbn_plan(MODE_FWD, d, dtype, pl), SSIP_ERR_ARG,
+               "ssip_conv_fwd_bnrelu_in: no LDS-DMA BN+ReLU-in plan");
+  SSIP_REQUIRE(z_out == nullptr || (d->R == 1 && d->S == 1 && d->pad == 0), SSIP_ERR_ARG,
+               "ssip_conv_fwd_bnrelu_in: z_out on the halo geometry and 1x1 convs only");
+  pl.args.zout = z_out;
   pl.args.A = y_in; pl.args.B = w_krsc; pl.args.out = y; pl.args.partial = bn_partial;
   pl.args.a_bytes = (uint32_t)((long)d->N * d->H * d->W * d->C * 2);
   pl.args.b_bytes = (uint32_t)((long)d->K * d->R * d->S * d->C * 2);

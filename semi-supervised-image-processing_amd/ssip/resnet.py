@@ -425,7 +425,12 @@ def _conv_bn(model: SSIPResNet, conv, bn, x: torch.Tensor, N, H, W, train: bool,
         nparts = ops.conv_fwd_partial_floats(g)
         partial = torch.empty(nparts, device=x.device, dtype=torch.float32)
         if in_bn is not None:
-            z = torch.empty_like(x) if (save and _BNRELU_Z) else None
+            # z_out: the halo forward writes it under SSIP_BNRELU_Z; a 1x1 conv
+            # on the LDS-DMA ring always does (its in-ring wgrad transform sits
+            # on the side stream's one-workgroup-per-CU grid and costs more
+            # than the stores: profiles/r6_bnrelu_in_glds_lab.txt)
+            one = g.R == 1 and g.S == 1
+            z = torch.empty_like(x) if (save and (_BNRELU_Z or one)) else None
             ops.conv_fwd_bnrelu_in(g, x, in_bn[0], in_bn[1], krsc, y, partial, z_out=z)
             if z is not None:
                 # the conv wrote relu(bn(x)) as it formed its tiles: the weight

@@ -65,6 +65,13 @@ def test_glds_bnrelu_in_matches_apply_then_conv_and_torch(dev, monkeypatch, name
     out = torch.empty((N, H, H, K), device=dev, dtype=DT)
     part = torch.zeros(nparts, device=dev)
     ops.conv_fwd_bnrelu_in(g, yh, sc, sh, krsc, out, part)
+    # 1x1: the same launch with z_out (the n-tile-0 workgroups store each
+    # transformed piece: z must be bn_apply's output, bit for bit)
+    zo = None
+    if R == 1:
+        zo = torch.full_like(yh, float("nan"))
+        out_z, part_z = torch.empty_like(out), torch.zeros(nparts, device=dev)
+        ops.conv_fwd_bnrelu_in(g, yh, sc, sh, krsc, out_z, part_z, z_out=zo)
     # apply pass + plain conv
     z = torch.empty_like(yh)
     ops.bn_apply(N * H * H, C, yh, sc, sh, None, True, z)
@@ -84,6 +91,9 @@ def test_glds_bnrelu_in_matches_apply_then_conv_and_torch(dev, monkeypatch, name
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int16), out2.view(torch.int16)), name
     assert torch.equal(part, part2), name
+    if zo is not None:
+        assert torch.equal(zo.view(torch.int16), z.view(torch.int16)), name
+        assert torch.equal(out_z.view(torch.int16), out.view(torch.int16)) and torch.equal(part_z, part), name
     for b, (d1, d2) in dws.items():
         assert torch.equal(d1, d2), (name, b)
     # vs torch fp32 on the same bf16 operands

@@ -164,7 +164,8 @@ int ssip_conv_wgrad_budget(const ssip_conv_desc* d, int dtype, const void* dy, c
  * another stream.
  * ABI 14: also bf16 stride-1 convs on the LDS-DMA ring kernels with 64 <= C
  * <= 512 input channels -- 1x1 / pad 0 (the ResNet-50 Bottleneck's conv3 over
- * relu(bn2(y2)), $SSIP_BNRELU_GLDS bit 0, on by default) and 3x3 / pad 1
+ * relu(bn2(y2)), $SSIP_BNRELU_GLDS bit 0, on by default from
+ * $SSIP_BNRELU_GLDS_MINM = 262144 rows N*H*W up) and 3x3 / pad 1
  * (bit 1, off: slower in the steps): each wave transforms
  * the input pieces it DMA'd once they land, before the k-step's barrier;
  * padding taps and rows past the grid stay zero.  Same bits as ssip_bn_apply

@@ -4009,6 +4009,13 @@ static bool glds_inbn_plan(int mode, const ssip_conv_desc* d, int dtype, Plan& p
   if (dtype != SSIP_BF16 || !desc_ok(d) || d->stride != 1 || d->C % 64 || d->C > GLDS_INBN_C || d->K % 64)
     return false;
   const int m = bnrelu_glds_mask();
+  // the 1x1 form pays where the apply pass it removes is large: per launch it
+  // wins at ResNet-50 layers 1-2 (>= 262,144 rows) and loses at layers 3-4,
+  // where the conv is short and the in-ring transform is not hidden
+  // (profiles/r6_bnrelu_in_glds_lab.txt); SSIP_BNRELU_GLDS_MINM overrides
+  const char* me = getenv("SSIP_BNRELU_GLDS_MINM");
+  const long min_rows = me != nullptr ? atol(me) : 262144l;
+  if (d->R == 1 && (long)d->N * d->H * d->W < min_rows) return false;
   const bool g1 = d->R == 1 && d->S == 1 && d->pad == 0 && (m & 1);
   const bool g3 = d->R == 3 && d->S == 3 && d->pad == 1 && (m & 2);
   if (!g1 && !g3) return false;

@@ -42,6 +42,8 @@ CASES = [
 @pytest.mark.parametrize("name,N,H,C,K,R,env", CASES, ids=[c[0] for c in CASES])
 def test_glds_bnrelu_in_matches_apply_then_conv_and_torch(dev, monkeypatch, name, N, H, C, K, R, env):
     monkeypatch.setenv("SSIP_BNRELU_GLDS", env)
+    # every shape, also those below the production row threshold
+    monkeypatch.setenv("SSIP_BNRELU_GLDS_MINM", "0")
     # the plain wgrad on the budget's plain tiles, as the INBN form plans (the
     # wide SSIP_WGRAD_BIG tiles have no INBN form): the same splits, same bits
     monkeypatch.setenv("SSIP_WGRAD_BIG", "0")
